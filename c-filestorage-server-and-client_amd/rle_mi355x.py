@@ -1,0 +1,157 @@
+"""ctypes binding of librle_mi355x.so — the MI355X RLE block codec.
+
+Mirrors the reference codec interface (samul-1/C-FileStorage-Server-and-Client
+include/rleCompression.h:4-5, src/rleCompression.c:9-62): `compress` / `decompress`
+call the drop-in RLEcompress / RLEdecompress exactly as src/filesystemApi.c does, and the
+`*_batch` functions expose the batched device-resident API of include/rle_mi355x.h on
+torch device tensors (PyTorch is only the allocator/stream plumbing here).
+
+The library is required: there is no Python or CPU fallback.  Loading fails loudly when
+librle_mi355x.so has not been built (`python -c "import __graft_entry__ as g; g.build()"`).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librle_mi355x.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
+
+RLE_OK = 0
+RLE_STATUS_OK = 0
+RLE_STATUS_OVERFLOW = 1
+RLE_STATUS_MISALIGNED = 2
+RLE_STATUS_SERIAL = 0x100
+
+_u64p = ctypes.c_void_p
+_lib = None
+_libc = ctypes.CDLL("libc.so.6")
+_libc.free.argtypes = [ctypes.c_void_p]
+
+
+class RLEError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the codec library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RLEError(f"{LIB_PATH} is missing: the HIP codec has not been built")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
+    L.rle_max_compressed_size.restype = sz
+    L.rle_max_compressed_size.argtypes = [sz]
+    L.rle_encode_batch_device.restype = ctypes.c_int
+    L.rle_encode_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.rle_decode_batch_device.restype = ctypes.c_int
+    L.rle_decode_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.rle_gen_synthetic_device.restype = ctypes.c_int
+    L.rle_gen_synthetic_device.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+    L.rle_mi355x_selftest.restype = ctypes.c_int
+    L.rle_mi355x_selftest.argtypes = []
+    L.rle_mi355x_device_count.restype = ctypes.c_int
+    L.rle_mi355x_device_count.argtypes = []
+    L.rle_mi355x_version.restype = ctypes.c_char_p
+    L.rle_mi355x_version.argtypes = []
+    L.RLEcompress.restype = ctypes.c_void_p
+    L.RLEcompress.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.RLEdecompress.restype = ctypes.c_void_p
+    L.RLEdecompress.argtypes = [ctypes.c_char_p, sz, sz, sz]
+    _lib = L
+    return L
+
+
+def max_compressed_size(U: int) -> int:
+    return int(lib().rle_max_compressed_size(U))
+
+
+def round16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+# ------------------------------------------------------------------ drop-in (host) API
+def compress(data: bytes) -> bytes:
+    """RLEcompress (src/rleCompression.c:9-45) through the drop-in C ABI."""
+    c = ctypes.c_size_t(0)
+    p = lib().RLEcompress(data, len(data), ctypes.byref(c))
+    if not p:
+        raise MemoryError("RLEcompress returned NULL")
+    out = ctypes.string_at(p, c.value) if c.value else b""
+    _libc.free(p)
+    return out
+
+
+def decompress(stream: bytes, U: int, E: int = 0) -> bytes:
+    """RLEdecompress (src/rleCompression.c:47-62): U decoded bytes followed by E zero bytes."""
+    p = lib().RLEdecompress(stream, len(stream), U, E)
+    if not p:
+        raise MemoryError("RLEdecompress returned NULL")
+    out = ctypes.string_at(p, U + E) if U + E else b""
+    _libc.free(p)
+    return out
+
+
+# ------------------------------------------------------------------ batch layout helpers
+def layout(sizes, align=16):
+    """Offsets of buffers packed back to back, each start 16-byte aligned; returns (offs, total)."""
+    offs, pos = [], 0
+    for s in sizes:
+        offs.append(pos)
+        pos += (int(s) + align - 1) // align * align
+    return offs, max(pos, align)
+
+
+def compressed_slots(sizes):
+    """Worst-case-capacity output slots for encoding buffers of the given sizes."""
+    return layout([max_compressed_size(int(s)) for s in sizes])
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None):
+    """Batched encode on device tensors (uint8 data; int64 offsets/lengths; int32 status)."""
+    n = in_off.numel()
+    rc = lib().rle_encode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                       _ptr(out_len), _ptr(status), n, _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_encode_batch_device failed: {rc}")
+
+
+def decode_batch(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, status=None, stream=None):
+    """Batched decode on device tensors."""
+    n = in_off.numel()
+    rc = lib().rle_decode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                       _ptr(out_len), _ptr(out_cap), _ptr(status), n, _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_decode_batch_device failed: {rc}")
+
+
+def gen_synthetic(d_out, off, length, kind=None, index=None, stream=None):
+    n = off.numel()
+    rc = lib().rle_gen_synthetic_device(_ptr(d_out), _ptr(off), _ptr(length), _ptr(kind), _ptr(index), n,
+                                        _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_gen_synthetic_device failed: {rc}")
+
+
+def selftest() -> int:
+    return int(lib().rle_mi355x_selftest())
+
+
+def device_count() -> int:
+    return int(lib().rle_mi355x_device_count())
+
+
+def version() -> str:
+    return lib().rle_mi355x_version().decode()

@@ -1,0 +1,80 @@
+/*
+ * rle_mi355x.h — batched, device-resident entry points of the MI355X RLE block codec.
+ *
+ * These are the batch forms of the reference codec (src/rleCompression.c:9-62, declared at
+ * include/rleCompression.h:4-5 of samul-1/C-FileStorage-Server-and-Client): the same token
+ * grammar, byte-identical output, applied to B independent buffers in one launch.  The
+ * reference has no batch API; its natural batch is readNFilesHandler's decode loop
+ * (src/filesystemApi.c:680-687), and the eviction decode loop (src/server.c:314-323).
+ *
+ * All pointers named d_* are device (HBM) pointers; `stream` is a hipStream_t passed as
+ * void* (NULL = the default stream).  Calls are asynchronous on that stream.  Return value:
+ * RLE_OK, or a negative RLE_E_* host-side error (nothing was launched).
+ *
+ * Layout rules:
+ *  - buffer i occupies d_in + d_in_off[i] .. + d_in_len[i]; d_in + d_in_off[i] and
+ *    d_out + d_out_off[i] must be 16-byte aligned (else d_status[i] = RLE_STATUS_MISALIGNED
+ *    and that buffer is skipped);
+ *  - encode: the output slot of buffer i must hold rle_max_compressed_size(d_in_len[i])
+ *    bytes; exactly d_out_len[i] = C bytes are written;
+ *  - decode: d_in_len[i] = C (compressed), d_out_len[i] = U (decoded size, as the reference's
+ *    uncompressedSize).  d_out_cap[i] (NULL: = U) is the writable slot size, U <= cap; the
+ *    first U bytes are always written.  Bytes of a slot past U are written only for streams
+ *    the encoder never emits and only where the reference would write them (its
+ *    extraAllocation region).
+ */
+#ifndef RLE_MI355X_H
+#define RLE_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* host-side return codes */
+#define RLE_OK          0
+#define RLE_E_INVAL    (-1)   /* bad argument */
+#define RLE_E_HIP      (-2)   /* a HIP runtime call failed */
+#define RLE_E_NODEV    (-3)   /* no usable gfx950 device */
+
+/* per-buffer status bits (d_status[i]) */
+#define RLE_STATUS_OK          0u
+#define RLE_STATUS_OVERFLOW    1u      /* decode: stream writes past cap (reference: heap overflow); truncated */
+#define RLE_STATUS_MISALIGNED  2u      /* input or output slot not 16-byte aligned; buffer skipped */
+#define RLE_STATUS_SERIAL      0x100u  /* info: stream decoded by the exact serial path (not encoder output) */
+
+/* Worst-case compressed size of U bytes (every run of length 2: 3 bytes per 2 input bytes). */
+size_t rle_max_compressed_size(size_t U);
+
+/* Batched encode (RLEcompress, src/rleCompression.c:9-45) of n buffers.
+ * d_status may be NULL. */
+int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                            void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                            uint32_t* d_status, uint32_t n, void* stream);
+
+/* Batched decode (RLEdecompress, src/rleCompression.c:47-62) of n buffers.
+ * d_out_cap and d_status may be NULL. */
+int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                            void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                            const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n, void* stream);
+
+/* Synthetic batch generator: xorshift64 (13,7,17), state seed
+ * 0x9E3779B97F4A7C15 + index, one step per byte; kind 0 zero, 1 random, 2 runs50,
+ * 3 runs90, 4 pairs.  d_kind / d_index may be NULL (kind 1, index = i). */
+int rle_gen_synthetic_device(void* d_out, const uint64_t* d_off, const uint64_t* d_len,
+                             const uint32_t* d_kind, const uint64_t* d_index, uint32_t n, void* stream);
+
+/* Runs the cross-lane (DPP) primitive self-test on the current device; 0 = pass. */
+int rle_mi355x_selftest(void);
+
+/* Number of visible HIP devices (0 when none). */
+int rle_mi355x_device_count(void);
+
+const char* rle_mi355x_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,95 @@
+"""CPU tests of the drop-in boundary: librle_mi355x.so loads and exports every function the
+headers in include/ declare; the drop-in header is plain C99 (as the reference's callers compile
+it, Makefile:6) and declares the reference prototypes (include/rleCompression.h:4-5)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+import rle_mi355x as R
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(REPO, "include")
+
+
+def declared_functions():
+    names = set()
+    for fn in os.listdir(INC):
+        if not fn.endswith(".h"):
+            continue
+        src = open(os.path.join(INC, fn)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = R.lib()
+    names = declared_functions()
+    assert {"RLEcompress", "RLEdecompress", "rle_encode_batch_device", "rle_decode_batch_device"} <= names
+    for n in sorted(names):
+        assert hasattr(L, n), f"librle_mi355x.so does not export {n}"
+
+
+def test_host_only_entry_points():
+    assert R.max_compressed_size(0) == 0
+    assert R.max_compressed_size(1) == 1
+    assert R.max_compressed_size(2) == 3
+    assert R.max_compressed_size(4096) == 6144
+    assert "gfx950" in R.version()
+    assert R.device_count() >= 0
+
+
+def test_reference_prototypes_exact():
+    src = open(os.path.join(INC, "rleCompression.h")).read()
+    assert "char* RLEcompress(char* data, size_t origSize, size_t* compressedSize);" in src
+    assert ("char* RLEdecompress(char* data, size_t compressedSize, size_t uncompressedSize, "
+            "size_t extraAllocation);") in src
+
+
+def test_headers_compile_as_c99():
+    code = '#include "rleCompression.h"\n#include "rle_mi355x.h"\nint main(void){size_t c=0;(void)c;' \
+           'char*(*f)(char*,size_t,size_t*)=RLEcompress;char*(*g)(char*,size_t,size_t,size_t)=RLEdecompress;' \
+           '(void)f;(void)g;return 0;}\n'
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "t.c")
+        open(p, "w").write(code)
+        r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I", INC, "-c", p, "-o",
+                            os.path.join(d, "t.o")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_c_caller_links_against_dropin():
+    """A C caller shaped like src/filesystemApi.c's write path links against the .so unchanged."""
+    code = r'''
+#include <stdlib.h>
+#include <string.h>
+#include "rleCompression.h"
+int append(char* content, size_t cs, size_t us, const char* add, size_t n, size_t* newcs, char** out) {
+    char* d = RLEdecompress(content, cs, us, n);
+    memcpy(d + us, add, n);
+    *out = RLEcompress(d, us + n, newcs);
+    free(d);
+    return 0;
+}
+int main(void) { return 0; }
+'''
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "caller.c")
+        open(p, "w").write(code)
+        r = subprocess.run(["gcc", "-std=c99", "-Wall", "-I", INC, p, "-o", os.path.join(d, "caller"),
+                            R.LIB_PATH, "-Wl,-rpath," + os.path.dirname(R.LIB_PATH)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_no_oracle_in_product_library():
+    """The product .so must not link or embed the CPU oracle."""
+    out = subprocess.run(["nm", "-D", R.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle_" not in out
+    ldd = subprocess.run(["ldd", R.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd and "librle_ref" not in ldd

@@ -1,0 +1,277 @@
+"""GPU parity tests: the HIP codec (through librle_mi355x.so's C ABI) against the oracle, the
+golden vectors of the compiled reference and the reference fixture pins.  Bit-exact everywhere.
+
+Slots are poisoned before each launch so a write past C (encode) or past U (decode) shows up."""
+import hashlib
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import rle_mi355x as R
+import rle_oracle as O
+from conftest import committed_file_bytes
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+POISON = 0xA5
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def _i64(vals):
+    return torch.tensor(np.asarray(vals, dtype=np.int64), device=DEV)
+
+
+def gpu_encode(bufs):
+    """Encode a list of byte strings in ONE batched launch; returns (outputs, status)."""
+    n = len(bufs)
+    sizes = [len(b) for b in bufs]
+    in_offs, in_total = R.layout(sizes)
+    host = np.zeros(in_total, np.uint8)
+    for b, o in zip(bufs, in_offs):
+        host[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    out_offs, out_total = R.compressed_slots(sizes)
+    d_in = torch.from_numpy(host).to(DEV)
+    d_out = torch.full((out_total + 16,), POISON, dtype=torch.uint8, device=DEV)
+    out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
+    status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
+    R.encode_batch(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    lens = out_len.cpu().numpy()
+    res = []
+    for i in range(n):
+        o, c = out_offs[i], int(lens[i])
+        res.append(out[o:o + c].tobytes())
+        cap_end = out_offs[i + 1] if i + 1 < n else out_total
+        assert (out[o + c:cap_end] == POISON).all(), f"encode wrote past C in buffer {i}"
+    return res, status.cpu().numpy()
+
+
+def gpu_decode(streams, usizes, caps=None, poison=True):
+    n = len(streams)
+    caps = caps if caps is not None else list(usizes)
+    in_offs, in_total = R.layout([len(s) for s in streams])
+    host = np.zeros(in_total, np.uint8)
+    for s, o in zip(streams, in_offs):
+        host[o:o + len(s)] = np.frombuffer(s, np.uint8)
+    out_offs, out_total = R.layout(caps)
+    d_in = torch.from_numpy(host).to(DEV)
+    d_out = torch.full((out_total + 16,), POISON if poison else 0, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
+    R.decode_batch(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out, _i64(out_offs), _i64(usizes),
+                   _i64(caps), status)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    res = [out[o:o + c].tobytes() for o, c in zip(out_offs, caps)]
+    return res, status.cpu().numpy()
+
+
+def test_selftest_dpp_primitives():
+    assert R.selftest() == 0
+
+
+def test_golden_vectors_encode_decode(vectors):
+    cases = [v for g in ("kat", "edge", "ladder", "fuzz") for v in vectors[g]]
+    xs = [bytes.fromhex(v["in"]) for v in cases]
+    ys = [bytes.fromhex(v["out"]) for v in cases]
+    got, st = gpu_encode(xs)
+    assert (st == 0).all()
+    bad = [i for i in range(len(xs)) if got[i] != ys[i]]
+    assert not bad, (len(bad), cases[bad[0]], got[bad[0]].hex())
+    dec, st = gpu_decode(ys, [len(x) for x in xs])
+    bad = [i for i in range(len(xs)) if dec[i] != xs[i]]
+    assert not bad, (len(bad), cases[bad[0]], dec[bad[0]].hex())
+    assert ((st & 0xFF) == 0).all()
+
+
+def test_invalid_streams_match_reference(vectors):
+    cases = vectors["invalid_decode"]
+    streams = [bytes.fromhex(v["in"]) for v in cases]
+    us = [v["U"] for v in cases]
+    caps = [v["U"] + v["E"] for v in cases]
+    dec, st = gpu_decode(streams, us, caps, poison=False)
+    bad = [i for i in range(len(cases)) if dec[i] != bytes.fromhex(cases[i]["out"])]
+    assert not bad, (len(bad), cases[bad[0]], dec[bad[0]].hex())
+    assert ((st & 0xFF) == 0).all()
+
+
+def test_decode_overflow_status():
+    dec, st = gpu_decode([b"aa9" * 3, b"aa9"], [2, 9], [2, 9])
+    assert st[0] & R.RLE_STATUS_OVERFLOW and dec[0] == b"aa"
+    assert st[1] == 0 and dec[1] == b"a" * 9
+
+
+def test_synthetic_pins_and_device_generator(vectors):
+    cases = [v for v in vectors["synthetic"]]
+    n = len(cases)
+    sizes = [v["U"] for v in cases]
+    offs, total = R.layout(sizes)
+    d = torch.zeros(total, dtype=torch.uint8, device=DEV)
+    R.gen_synthetic(d, _i64(offs), _i64(sizes), torch.tensor([v["kind"] for v in cases], dtype=torch.int32,
+                                                              device=DEV), _i64([v["index"] for v in cases]))
+    torch.cuda.synchronize()
+    h = d.cpu().numpy()
+    xs = [h[o:o + s].tobytes() for o, s in zip(offs, sizes)]
+    for x, v in zip(xs, cases):
+        assert sha(x) == v["sha_in"], v
+    got, st = gpu_encode(xs)
+    for y, v in zip(got, cases):
+        assert len(y) == v["C"] and sha(y) == v["sha_out"], v
+    dec, st = gpu_decode(got, sizes)
+    assert all(a == b for a, b in zip(dec, xs)) and ((st & 0xFF) == 0).all()
+
+
+def _oracle_parity(xs):
+    ys, st = gpu_encode(xs)
+    assert (st == 0).all()
+    for i, x in enumerate(xs):
+        ref = O.encode(x)
+        assert ys[i] == ref, (i, len(x), len(ys[i]), len(ref))
+    dec, st = gpu_decode(ys, [len(x) for x in xs])
+    for i, x in enumerate(xs):
+        assert dec[i] == x, (i, len(x))
+    assert ((st & 0xFF) == 0).all()
+    return ys
+
+
+def test_config1_4096x4k_roundtrip():
+    # BASELINE configs[1]: 4096 synthetic 4 KiB buffers (random / zero), bit-exact vs CPU
+    xs = [O.gen(1 if i % 2 == 0 else 0, i, 4096) for i in range(4096)]
+    _oracle_parity(xs)
+
+
+def test_ragged_sizes_and_tile_edges():
+    sizes = list(range(0, 130)) + [1023, 1024, 1025, 1026, 1039, 2047, 2048, 2049, 3071, 3072, 4095, 4096, 4097,
+                                   8191, 8193, 16383, 16385]
+    xs = []
+    for k in range(5):
+        for i, s in enumerate(sizes):
+            xs.append(O.gen(k, 1000 + i, s))
+    rng = np.random.default_rng(3)
+    for i in range(300):  # digit-heavy and repeat-heavy content around tile edges
+        s = int(rng.integers(900, 2300))
+        alpha = np.frombuffer(rng.choice([b"a0123456789", b"\0\x01", b"33", b"ab"]), np.uint8)
+        runs = rng.integers(1, 22, size=s)
+        vals = rng.choice(alpha, size=s)
+        xs.append(np.repeat(vals, runs)[:s].tobytes())
+    _oracle_parity(xs)
+
+
+def test_long_runs_across_tiles():
+    xs = [bytes(1 << 20), b"\xff" * 100000, b"a" * 9 * 1024, b"a" * (9 * 1024 + 1), b"\0" * 1023 + b"a" * 3000,
+          O.gen(3, 5, 1 << 20), O.gen(4, 5, 300001), O.gen(2, 6, 777777)]
+    _oracle_parity(xs)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_64k_batch_per_kind(kind):
+    xs = [O.gen(kind, i, 65536) for i in range(512)]
+    _oracle_parity(xs)
+
+
+def test_mixed_sizes_batch():
+    xs = []
+    for i in range(160):
+        s = np.random.default_rng(i).integers(0, 9)
+        U = (1 << (12 + int(s))) + (int(np.random.default_rng(i + 99).integers(0, 4096)) if i % 2 else 0)
+        xs.append(O.gen(i % 4, i, U))
+    _oracle_parity(xs)
+
+
+def test_reference_fixture_files(dummyfiles):
+    xs, pins = [], []
+    for e in dummyfiles["files"]:
+        x = committed_file_bytes(e)
+        if x is not None:
+            xs.append(x)
+            pins.append(e)
+    ys, st = gpu_encode(xs)
+    for y, e in zip(ys, pins):
+        assert len(y) == e["C"] and sha(y) == e["sha_out"], e["path"]
+    dec, st = gpu_decode(ys, [len(x) for x in xs])
+    assert all(a == b for a, b in zip(dec, xs))
+
+
+def test_dropin_compress_decompress(dummyfiles):
+    assert R.compress(b"aaaaaaaaaaaab") == b"aa9aa3b"
+    assert R.compress(b"") == b""
+    assert R.decompress(b"", 0) == b""
+    assert R.decompress(b"", 5, 3) == bytes(8)
+    assert R.compress(b"\0") == b"\0" and R.decompress(b"\0", 1) == b"\0"
+    for e in dummyfiles["files"]:
+        x = committed_file_bytes(e)
+        if x is None:
+            continue
+        y = R.compress(x)
+        assert len(y) == e["C"] and sha(y) == e["sha_out"], e["path"]
+        # write path (src/filesystemApi.c:767-774): decode with E extra zero bytes, append, re-encode
+        z = R.decompress(y, len(x), 1000)
+        assert z[:len(x)] == x and z[len(x):] == bytes(1000)
+        z = z[:len(x)] + b"tail-bytes" * 100
+        assert R.compress(z) == O.encode(z)
+
+
+def test_dropin_concurrent_threads():
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(t)
+        for k in range(40):
+            U = int(rng.integers(0, 200000))
+            x = O.gen(int(rng.integers(0, 5)), t * 1000 + k, U)
+            y = R.compress(x)
+            if y != O.encode(x):
+                errors.append(("enc", t, k, U))
+            if R.decompress(y, U) != x:
+                errors.append(("dec", t, k, U))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_misaligned_slot_is_rejected():
+    d_in = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    d_out = torch.zeros(128, dtype=torch.uint8, device=DEV)
+    st = torch.full((1,), 0, dtype=torch.int32, device=DEV)
+    out_len = torch.zeros(1, dtype=torch.int64, device=DEV)
+    R.encode_batch(d_in, _i64([3]), _i64([10]), d_out, _i64([0]), out_len, st)
+    torch.cuda.synchronize()
+    assert int(st.item()) == R.RLE_STATUS_MISALIGNED
+
+
+def test_full_size_shard_roundtrip_property():
+    """configs[3] per-GPU shape at 1/8 scale (16384 x 64 KiB = 1 GiB): device round trip equal, a
+    strided sample (every 1021st buffer) bit-exact vs the oracle, and sum(C) of the sample."""
+    n, U = 16384, 65536
+    kinds = torch.tensor([i % 4 for i in range(n)], dtype=torch.int32, device=DEV)
+    offs = torch.arange(n, dtype=torch.int64, device=DEV) * U
+    lens = torch.full((n,), U, dtype=torch.int64, device=DEV)
+    d_in = torch.empty(n * U, dtype=torch.uint8, device=DEV)
+    R.gen_synthetic(d_in, offs, lens, kinds, None)
+    cap = R.round16(R.max_compressed_size(U))
+    d_c = torch.empty(n * cap, dtype=torch.uint8, device=DEV)
+    coffs = torch.arange(n, dtype=torch.int64, device=DEV) * cap
+    clen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    R.encode_batch(d_in, offs, lens, d_c, coffs, clen)
+    d_out = torch.empty(n * U, dtype=torch.uint8, device=DEV)
+    st = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
+    R.decode_batch(d_c, coffs, clen, d_out, offs, lens, None, st)
+    torch.cuda.synchronize()
+    assert torch.equal(d_out, d_in)
+    assert int((st & 0xFF).abs().sum().item()) == 0
+    cl = clen.cpu().numpy()
+    for i in range(0, n, 1021):
+        x = O.gen(i % 4, i, U)
+        y = O.encode(x)
+        assert cl[i] == len(y)
+        got = d_c[i * cap:i * cap + len(y)].cpu().numpy().tobytes()
+        assert got == y, i
