@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X RLE block codec (BASELINE.json metric: GiB/s RLE encode+decode,
+device-resident, batched).
+
+One step = one pass of the hot path over one batch resident in HBM: a batched encode launch
+(RLEcompress, src/rleCompression.c:9-45) followed by a batched decode launch of its output
+(RLEdecompress, src/rleCompression.c:47-62).  With N > 1 ranks (one process per GPU,
+torch.distributed over RCCL) the global batch is sharded round-robin (buffer i -> rank i % N)
+and each step also all-gathers the per-buffer compressed sizes over xGMI and scans them into
+global stream offsets; payloads never leave their GPU.
+
+value = uncompressed bytes round-tripped by all ranks / max-over-ranks wall time of K steps.
+Default workload: BASELINE configs[1], 4096 x 4 KiB synthetic buffers per GPU (random / zero).
+
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1|dec64k|mixed|cfg3]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "c-filestorage-server-and-client_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import rle_mi355x as R  # noqa: E402
+
+METRIC = "GiB/s RLE encode+decode, device-resident, batched 4–256 KiB buffers"
+GIB = float(1 << 30)
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def xs64(s):
+    s ^= (s << 13) & 0xFFFFFFFFFFFFFFFF
+    s ^= s >> 7
+    s ^= (s << 17) & 0xFFFFFFFFFFFFFFFF
+    return s
+
+
+def mixed_size(i):
+    """configs[2] size rule (same as oracle/ref_bench.c --size 0): log-uniform 4 KiB..1 MiB, half
+    of them with a non-power-of-two remainder."""
+    s = (0x9E3779B97F4A7C15 + i + 0x5151) & 0xFFFFFFFFFFFFFFFF
+    s = xs64(s)
+    r = s
+    U = 1 << (12 + r % 9)
+    if (r >> 8) & 1:
+        s = xs64(s)
+        U += (s >> 16) % U
+    return U
+
+
+WORKLOADS = {
+    # name: (buffers per GPU, size(global index) or fixed, kind(local index), description)
+    "cfg1": dict(n=4096, size=4096, kinds=(1, 0), ref_kinds="1,0",
+                 desc="configs[1]: 4096 x 4 KiB synthetic buffers per GPU (random / zero alternating), "
+                      "encode+decode round trip"),
+    "dec64k": dict(n=16384, size=65536, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
+                   desc="16384 x 64 KiB per GPU (zero / random / runs50 / runs90), encode+decode round trip"),
+    "mixed": dict(n=1024, size=None, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
+                  desc="configs[2]: 1024 mixed 4 KiB-1 MiB buffers per GPU (zero / random / runs50 / runs90)"),
+    "cfg3": dict(n=131072, size=65536, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
+                 desc="configs[3] shard: 131072 x 64 KiB per GPU (1 M x 64 KiB over 8 GPUs), round-robin"),
+}
+
+
+class Batch:
+    """One rank's shard of a synthetic batch, resident in HBM, with compressed and decoded slots."""
+
+    def __init__(self, wl, rank, world, dev):
+        n = wl["n"]
+        kinds = wl["kinds"]
+        gidx = [k * world + rank for k in range(n)]
+        sizes = [wl["size"] if wl["size"] else mixed_size(i) for i in gidx]
+        offs, total = R.layout(sizes)
+        coffs, ctotal = R.compressed_slots(sizes)
+        i64 = lambda v: torch.tensor(v, dtype=torch.int64, device=dev)
+        self.n = n
+        self.sizes = sizes
+        self.u_bytes = sum(sizes)
+        self.offs, self.lens = i64(offs), i64(sizes)
+        self.coffs = i64(coffs)
+        self.clen = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.status = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.d_in = torch.empty(total, dtype=torch.uint8, device=dev)
+        self.d_c = torch.empty(ctotal, dtype=torch.uint8, device=dev)
+        self.d_out = torch.empty(total, dtype=torch.uint8, device=dev)
+        kind_t = torch.tensor([kinds[k % len(kinds)] for k in range(n)], dtype=torch.int32, device=dev)
+        R.gen_synthetic(self.d_in, self.offs, self.lens, kind_t, i64(gidx))
+        torch.cuda.synchronize()
+
+    def encode(self, stream=None):
+        R.encode_batch(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status, stream=stream)
+
+    def decode(self, stream=None):
+        R.decode_batch(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
+                       stream=stream)
+
+
+def gather_global_offsets(clen, world):
+    """RCCL all-gather of the per-buffer compressed sizes, then the exclusive scan in global
+    (round-robin) order: global buffer i = k * world + rank."""
+    n = clen.numel()
+    g = torch.empty(world * n, dtype=clen.dtype, device=clen.device)
+    dist.all_gather_into_tensor(g, clen)
+    glob = g.view(world, n).t().reshape(-1)           # global order
+    return torch.cumsum(glob, 0) - glob               # exclusive scan
+
+
+def time_kernels(fn, reps, stream):
+    """Average duration of fn's launch, from HIP events on the stream the kernel runs on."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in evs) / reps * 1e-3
+
+
+def cpu_baseline(wl, seconds, threads, flavor):
+    """The reference codec (src/rleCompression.c compiled unchanged by oracle/Makefile) timed on this
+    host's cores on the same synthetic batch, repeated passes for a bounded sample."""
+    exe = os.path.join(REPO, "oracle", "_ref", f"ref_bench_{flavor}")
+    if not os.path.exists(exe):
+        return None
+    size = wl["size"] if wl["size"] else 0
+    cmd = [exe, "--kinds", wl["ref_kinds"], "--size", str(size), "--count", str(wl["n"]), "--threads",
+           str(threads), "--seconds", str(seconds)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 4 + 120)
+    if r.returncode != 0:
+        print(f"cpu baseline failed: {r.stderr}", file=sys.stderr)
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def load_pmc(workload):
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get(workload)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg1", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    wl = WORKLOADS[args.workload]
+    stream = torch.cuda.current_stream()
+
+    B = Batch(wl, rank, world, dev)
+
+    def step():
+        B.encode(stream)
+        if world > 1:
+            gather_global_offsets(B.clen, world)
+        B.decode(stream)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(B.d_out, B.d_in)) and int(B.status.abs().sum().item()) == 0
+    c_bytes = int(B.clen.sum().item())
+    u_local = B.u_bytes
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+        ut = torch.tensor([u_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(ut, op=dist.ReduceOp.SUM)
+        total_u = int(ut.item())
+    else:
+        total_u = u_local
+
+    # per-kernel durations (HIP events on the launch stream), algorithmic bytes = U + C per launch
+    reps = max(10, min(args.steps, 50))
+    t_enc = time_kernels(lambda: B.encode(stream), reps, stream)
+    t_dec = time_kernels(lambda: B.decode(stream), reps, stream)
+    alg = u_local + c_bytes
+    kern = {"encode": {"us": t_enc * 1e6, "GBps": alg / t_enc / 1e9},
+            "decode": {"us": t_dec * 1e6, "GBps": alg / t_dec / 1e9}}
+    dom = "encode" if t_enc >= t_dec else "decode"
+    pmc = load_pmc(args.workload)
+    traffic = pmc.get(dom) if isinstance(pmc, dict) else None
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(kern[dom]["GBps"], 2), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(kern[dom]["GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "alg_bytes_per_launch": alg}
+
+    north = None
+    if rank == 0 and world == 1 and not args.no_north_star and args.workload != "dec64k":
+        del B
+        torch.cuda.empty_cache()
+        N = Batch(WORKLOADS["dec64k"], 0, 1, dev)
+        N.encode(stream)
+        torch.cuda.synchronize()
+        nc = int(N.clen.sum().item())
+        td = time_kernels(lambda: N.decode(stream), 20, stream)
+        te = time_kernels(lambda: N.encode(stream), 20, stream)
+        nok = bool(torch.equal(N.d_out, N.d_in))
+        nalg = N.u_bytes + nc
+        north = {"workload": WORKLOADS["dec64k"]["desc"], "decode_us": td * 1e6,
+                 "decode_GBps": nalg / td / 1e9, "decode_frac": round(nalg / td / 1e9 / HBM_PEAK_GBPS, 4),
+                 "encode_GBps": nalg / te / 1e9, "u_bytes": N.u_bytes, "c_bytes": nc, "verified": nok}
+        del N
+        torch.cuda.empty_cache()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = min(16, os.cpu_count() or 1)
+        r0 = cpu_baseline(wl, args.cpu_seconds, threads, "O0")
+        r2 = cpu_baseline(wl, max(2.0, args.cpu_seconds / 2), threads, "O2")
+        if r0:
+            cpu = {"value": round(r0["rt_gibs"], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                   "sample": f"reference src/rleCompression.c compiled unchanged with its Makefile flags "
+                             f"(-Wall -g -std=c99), {threads} pthreads, repeated passes over the same batch for "
+                             f"{args.cpu_seconds:.0f} s ({r0['buffers']} buffers, {r0['u_bytes']} bytes)",
+                   "c_batch_match": r0["c_batch"] == c_bytes,
+                   "O2": round(r2["rt_gibs"], 4) if r2 else None}
+
+    if rank == 0:
+        value = total_u * args.steps / elapsed / GIB
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+               "config": {"workload": wl["desc"], "buffers_per_gpu": wl["n"],
+                          "buffer_bytes": wl["size"] or "mixed 4 KiB-2 MiB",
+                          "u_bytes_per_gpu": total_u // world, "c_bytes_rank0": c_bytes,
+                          "parallelism": f"shard round-robin over {world} GPU(s)" +
+                                         (", RCCL all-gather of sizes" if world > 1 else "")},
+               "verified_bit_exact_roundtrip": ok, "kernels": kern, "roofline": roofline, "cpu_baseline": cpu,
+               "north_star_dec64k": north}
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,13 +8,15 @@
 //           (signed char)y[j+2]-'0'-1 copies, capped at U      — src/rleCompression.c:50-60
 //
 // Execution model: one wave64 owns one buffer and walks it in 1 KiB tiles,
-// 16 bytes per lane (one global_load_dwordx4 per lane, two tiles prefetched ahead).  Run
-// boundaries / token starts are found with 16-bit per-lane masks built by SWAR byte compares;
-// the sequential state (encode: run phase mod 9; decode: token phase 0..2) and the output
-// offsets are carried across lanes with DPP wave scans (row_shr/row_bcast, no LDS round
-// trip) and across tiles in scalar registers.  Output bytes are staged in a per-wave LDS
-// ring (XOR-swizzled against bank conflicts) and leave as aligned, coalesced 16-byte stores.
-// No MFMA: this is an HBM-bound byte scan.
+// 16 bytes per lane.  Loads are range-checked buffer_load_dwordx4 kept three tiles deep in
+// registers; their completion is counted by hand (s_waitcnt vmcnt(N), N = the stores issued
+// since), because hipcc's own bookkeeping drains the queue at every loop header once a
+// variable number of stores sits in the loop.  Run boundaries and token starts are 16-bit
+// per-lane masks from SWAR byte compares; the sequential state (encode: run start position;
+// decode: token phase 0..2 as a v_perm byte map) and output offsets cross lanes by DPP wave
+// scans and cross tiles in scalar registers.  Each lane scatters its output into a per-wave
+// LDS staging area that is linear per tile, and complete 16-byte chunks leave as coalesced
+// buffer_store_dwordx4.  No MFMA: this is an HBM-bound byte scan.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,13 +24,19 @@
 
 namespace rle {
 
-constexpr uint32_t kWave = 64;
-constexpr uint32_t kWavesPerBlock = 4;
-constexpr uint32_t kBlock = kWave * kWavesPerBlock;
-constexpr uint32_t kTile = 1024;      // input bytes per wave step (16 per lane)
-constexpr uint32_t kEncRing = 2048;   // encode staging ring, bytes per wave (tile output <= 1.5 KiB + 15)
-constexpr uint32_t kDecRing = 4096;   // decode staging ring, positions per wave (tile output <= 3078 + 15)
-constexpr uint32_t kMaxBlocks = 8192;
+typedef uint32_t u32;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr u32 kWave = 64;
+constexpr u32 kWavesPerBlock = 4;
+constexpr u32 kBlock = kWave * kWavesPerBlock;
+constexpr u32 kTile = 1024;       // input bytes per wave step (16 per lane)
+constexpr u32 kEncRing = 2048;    // encode staging bytes per wave (tile output <= 1538 + 15)
+constexpr u32 kEncGuard = 16;     // non-start positions may write 2 bytes before the tile base
+constexpr u32 kDecRing = 3120;    // decode staging positions (u16) per wave: <= 194 chunks + partial
+constexpr u32 kMaxBlocks = 8192;
+constexpr u32 kMaxBufferBytes = 0x7FFFFFF0u;   // per-buffer limit (32-bit in-buffer offsets)
+constexpr u32 kOOB = 0x80000000u;               // store offset dropped by the range check
 
 // ---------------------------------------------------------------- cross-lane primitives (DPP)
 enum : int {
@@ -37,25 +45,19 @@ enum : int {
 };
 
 template <int kCtrl, int kRowMask = 0xf>
-__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t src) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, kCtrl, kRowMask, 0xf, false);
+__device__ __forceinline__ u32 dpp(u32 old, u32 src) {
+    return (u32)__builtin_amdgcn_update_dpp((int)old, (int)src, kCtrl, kRowMask, 0xf, false);
 }
-// value of lane-1 (lane 0 gets `fill`)
-__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t fill) { return dpp<kWaveShr1>(fill, v); }
-// value of lane+1 (lane 63 gets `fill`)
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t fill) { return dpp<kWaveShl1>(fill, v); }
-
-__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-__device__ __forceinline__ uint32_t uniform(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
+// value of lane-1 (lane 0 gets `fill`) / of lane+1 (lane 63 gets `fill`)
+__device__ __forceinline__ u32 from_prev_lane(u32 v, u32 fill) { return dpp<kWaveShr1>(fill, v); }
+__device__ __forceinline__ u32 from_next_lane(u32 v, u32 fill) { return dpp<kWaveShl1>(fill, v); }
+__device__ __forceinline__ u32 readlane(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
+__device__ __forceinline__ u32 uniform(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
 
 // Inclusive wave scan for an associative op(a_earlier, b_later) with identity `id`.
 // Must be called with all 64 lanes active.
 template <class Op>
-__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x, uint32_t id, Op op) {
+__device__ __forceinline__ u32 wave_scan_incl(u32 x, u32 id, Op op) {
     x = op(dpp<kRowShr1>(id, x), x);
     x = op(dpp<kRowShr2>(id, x), x);
     x = op(dpp<kRowShr4>(id, x), x);
@@ -65,31 +67,25 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x, uint32_t id, Op o
     return x;
 }
 struct OpAdd {
-    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return a + b; }
+};
+struct OpMax {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return a > b ? a : b; }
 };
 // "latest present value": values are 0 (absent) or 0x100|byte
 struct OpLatest {
-    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return b ? b : a; }
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return b ? b : a; }
 };
-__device__ __forceinline__ uint32_t mod9(uint32_t x) { return x >= 9u ? x - 9u : x; }  // x <= 17
-// Encode phase transfer functions: code >= 16 -> constant (code-16); code < 16 -> add code mod 9.
+// token-phase maps {0,1,2} -> {0,1,2} as v_perm selectors: byte d = image of d; byte 3 = 3
+constexpr u32 kMapId = 0x03020100u;
+struct OpMap {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return __builtin_amdgcn_perm(b, b, a); }
+};
+// encode phase transfer functions (self-test only): code >= 16 -> constant, else add mod 9
+__device__ __forceinline__ u32 mod9s(u32 x) { return x >= 9u ? x - 9u : x; }
 struct OpPhase9 {
-    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const {
-        return b >= 16u ? b : (a >= 16u ? 16u + mod9(a - 16u + b) : mod9(a + b));
-    }
-};
-__device__ __forceinline__ uint32_t apply9(uint32_t f, uint32_t q) { return f >= 16u ? f - 16u : mod9(q + f); }
-// Decode token-phase maps {0,1,2} -> {0,1,2}, 2 bits per entry; identity = 0b100100.
-constexpr uint32_t kMap3Id = 0u | (1u << 2) | (2u << 4);
-struct OpMap3 {
-    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const {
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t d = 0; d < 3; ++d) {
-            const uint32_t x = (a >> (2 * d)) & 3u;
-            r |= ((b >> (2 * x)) & 3u) << (2 * d);
-        }
-        return r;
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const {
+        return b >= 16u ? b : (a >= 16u ? 16u + mod9s(a - 16u + b) : mod9s(a + b));
     }
 };
 
@@ -100,123 +96,214 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // ---------------------------------------------------------------- byte SWAR helpers
-// bit k (k=0..3) set iff byte k of d is non-zero
-__device__ __forceinline__ uint32_t nz4(uint32_t d) {
-    const uint32_t t = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
-    return ((t >> 7) * 0x10204080u) >> 28;
+// bit k (k = 0..3) set iff byte k of d is non-zero
+__device__ __forceinline__ u32 nz4(u32 d) {
+    u32 t = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+    t >>= 7;             // bytes' flags at bits 0, 8, 16, 24
+    t |= t >> 7;         // ... at bits 0, 1 and 16, 17
+    return (t | (t >> 14)) & 0xFu;
 }
-__device__ __forceinline__ uint32_t lowmask(uint32_t nbits) { return nbits >= 32u ? ~0u : ((1u << nbits) - 1u); }
-__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[4], uint32_t j) {  // j compile-time after unroll
-    return (w[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
-}
-
-// LDS ring swizzle: XOR dword-in-32B-group with the 128-B line index (bits 2..4 ^= bits 7..9).
-__device__ __forceinline__ uint32_t swz(uint32_t a) { return a ^ (((a >> 7) & 7u) << 2); }
-
-__device__ __forceinline__ void cswap(uint32_t& a, uint32_t& b, bool c) {
-    const uint32_t ta = c ? b : a, tb = c ? a : b;
-    a = ta; b = tb;
-}
-// out[k] = in[k ^ m] for 4 dwords
-__device__ __forceinline__ uint4 perm4(uint4 v, uint32_t m) {
-    cswap(v.x, v.y, m & 1u); cswap(v.z, v.w, m & 1u);
-    cswap(v.x, v.z, m & 2u); cswap(v.y, v.w, m & 2u);
-    return v;
+__device__ __forceinline__ u32 lowmask(u32 nbits) { return nbits >= 32u ? ~0u : ((1u << nbits) - 1u); }
+__device__ __forceinline__ u32 alignbyte(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
+__device__ __forceinline__ u32 bfe(u32 v, u32 off, u32 w) { return __builtin_amdgcn_ubfe(v, off, w); }
+__device__ __forceinline__ u32 bcnt(u32 v, u32 acc) { return (u32)__builtin_popcount(v) + acc; }
+// 4-bit mask -> bytes 0x01
+__device__ __forceinline__ u32 nib_to_bytes(u32 n) { return (n * 0x00204081u) & 0x01010101u; }
+__device__ __forceinline__ u32 mod9(u32 x) {
+    const u32 q = __umulhi(x, 0x38E38E39u) >> 1;
+    return x - 9u * q;
 }
 
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* base, uint64_t len, uint64_t off) {
-    if (off < len) return *reinterpret_cast<const uint4*>(base + off);
-    return make_uint4(0u, 0u, 0u, 0u);
+// ---------------------------------------------------------------- memory pipeline (hand-counted)
+// 128-bit buffer resource (raw buffer, stride 0): loads past num_records return 0, stores past
+// it are dropped.  Built from wave-uniform values only.
+__device__ __forceinline__ u32x4 make_rsrc(const void* base, u32 nbytes) {
+    const uint64_t a = (uint64_t)base;
+    u32x4 r;
+    r.x = (u32)a;
+    r.y = (u32)(a >> 32) & 0xFFFFu;
+    r.z = nbytes;
+    r.w = 0x00020000u;
+    return r;
+}
+// LDS byte address of a __shared__ pointer
+__device__ __forceinline__ u32 lds_addr(const void* p) {
+    return (u32)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// Loads and stores in asm: hipcc neither counts nor waits for them; vm_wait() is the only wait
+// for them.  Loads go straight to LDS (LDS-DMA: lane i's 16 bytes land at lds + 16 i), so no
+// VGPR is in flight that the compiler could copy or reuse before the data lands.
+__device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
+    u32 keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"   // earlier ds_reads of this slot have completed
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(lds), "s"(rs)
+        : "memory");
+}
+__device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v) {
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+// wait until at most n vector-memory ops are outstanding
+#define RLE_VMW(N)                                            \
+    case N:                                                   \
+        asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+        break;
+__device__ __forceinline__ void vm_wait(u32 n) {
+    switch (n < 12u ? n : 12u) {
+        RLE_VMW(0) RLE_VMW(1) RLE_VMW(2) RLE_VMW(3) RLE_VMW(4) RLE_VMW(5) RLE_VMW(6)
+        RLE_VMW(7) RLE_VMW(8) RLE_VMW(9) RLE_VMW(10) RLE_VMW(11) RLE_VMW(12)
+        default: break;
+    }
+}
+#undef RLE_VMW
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Walk one buffer's tiles with loads three tiles deep into three LDS slots (1 KiB each),
+// rotating slots by unrolling.  step(t, cur, nxt) processes tile t from slot `cur` (nxt = slot
+// of tile t+1, its lookahead) and returns the number of store instructions it issued, or ~0u
+// to stop early.  The wait before a step counts those stores: they are younger than the load
+// it needs.
+template <class Step>
+__device__ __forceinline__ void walk_tiles(u32x4 rs, u32 ntiles, u32 lane, const uint8_t* slots, Step step) {
+    const u32 lo = 16u * lane;
+    const uint8_t* s0 = slots;
+    const uint8_t* s1 = slots + kTile;
+    const uint8_t* s2 = slots + 2 * kTile;
+    const u32 l0 = uniform(lds_addr(s0)), l1 = l0 + kTile, l2 = l0 + 2 * kTile;
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
+    dma_tile(rs, lo, l0);
+    dma_tile(rs, kTile + lo, l1);
+    dma_tile(rs, 2 * kTile + lo, l2);
+    u32 prev = 0;
+    for (u32 t = 0; t < ntiles; t += 3) {
+        vm_wait(prev + 1);
+        prev = step(t, s0, s1);
+        if (prev == ~0u || t + 1 >= ntiles) break;
+        dma_tile(rs, (t + 3) * kTile + lo, l0);
+        vm_wait(prev + 1);
+        prev = step(t + 1, s1, s2);
+        if (prev == ~0u || t + 2 >= ntiles) break;
+        dma_tile(rs, (t + 4) * kTile + lo, l1);
+        vm_wait(prev + 1);
+        prev = step(t + 2, s2, s0);
+        if (prev == ~0u) break;
+        dma_tile(rs, (t + 5) * kTile + lo, l2);
+    }
+    vm_drain();
 }
 
 // ================================================================ ENCODE
 struct EncState {
-    uint64_t out_pos;   // compressed bytes produced so far
-    uint64_t flushed;   // compressed bytes already stored to HBM (multiple of 16)
-    uint32_t prev_byte; // input byte at tile_pos-1
-    uint32_t q;         // run phase ((i - runstart) mod 9) of input byte tile_pos-1
+    u32 out_pos;    // compressed bytes produced so far
+    u32 flushed;    // compressed bytes already stored (multiple of 16); staging base
+    u32 prev_top;   // input byte at tile_pos-1, in bits 24..31
+    u32 rs;         // start position of the run holding input byte tile_pos-1
 };
 
-__device__ __forceinline__ void enc_tile(const uint4 cur, const uint4 nxt, uint64_t pos, uint64_t U,
-                                         uint32_t lane, uint8_t* ring, uint8_t* dst, EncState& st) {
-    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
-    const uint64_t p0 = pos + 16u * lane;
-    const uint32_t nl = p0 >= U ? 0u : (uint32_t)((U - p0) < 16u ? (U - p0) : 16u);
-    const uint32_t validm = lowmask(nl);
+__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const uint8_t* nslot, u32 pos, u32 U, u32 lane,
+                                        uint8_t* stage, u32x4 rso, EncState& st) {
+    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    const uint2 nx = *reinterpret_cast<const uint2*>(nslot);
+    const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+    const u32 p0 = pos + 16u * lane;
+    const u32 nl = p0 < U ? ((U - p0) < 16u ? (U - p0) : 16u) : 0u;
+    const u32 validm = lowmask(nl);
 
-    // run boundaries: bit j <=> x[p0+j] != x[p0+j-1] (or p0+j == 0); virtual boundaries past U
-    const uint32_t last = w[3] >> 24;
-    const uint32_t prevb = from_prev_lane(last, st.prev_byte);
-    uint32_t B = nz4(w[0] ^ ((w[0] << 8) | prevb)) | (nz4(w[1] ^ ((w[1] << 8) | (w[0] >> 24))) << 4) |
-                 (nz4(w[2] ^ ((w[2] << 8) | (w[1] >> 24))) << 8) | (nz4(w[3] ^ ((w[3] << 8) | (w[2] >> 24))) << 12);
-    if (p0 == 0) B |= 1u;
+    // run boundaries: bit j <=> x[p0+j] != x[p0+j-1] (or p0+j == 0); positions >= U count as
+    // boundaries (they end the last run)
+    const u32 top = w[3] & 0xFF000000u;
+    const u32 ptop = from_prev_lane(top, st.prev_top);
+    u32 B = nz4(w[0] ^ alignbyte(w[0], ptop, 3)) | (nz4(w[1] ^ alignbyte(w[1], w[0], 3)) << 4) |
+            (nz4(w[2] ^ alignbyte(w[2], w[1], 3)) << 8) | (nz4(w[3] ^ alignbyte(w[3], w[2], 3)) << 12);
+    B |= (p0 == 0u) ? 1u : 0u;
     B |= ~validm & 0xFFFFu;
 
-    // 8-byte lookahead (for the repeat count): next lane's boundaries; lane 63 reads the next tile
-    const uint32_t nx0 = readlane(nxt.x, 0), nx1 = readlane(nxt.y, 0), last63 = readlane(last, 63);
-    const uint64_t pn = pos + kTile;
-    const uint32_t nvn = pn >= U ? 0u : (uint32_t)((U - pn) < 8u ? (U - pn) : 8u);
-    const uint32_t B8 = (nz4(nx0 ^ ((nx0 << 8) | last63)) | (nz4(nx1 ^ ((nx1 << 8) | (nx0 >> 24))) << 4) |
-                         (~lowmask(nvn))) & 0xFFu;
-    const uint32_t B24 = B | ((from_next_lane(B, B8) & 0xFFu) << 16);
+    // boundaries of the next 8 bytes (repeat-count lookahead); lane 63 reads the next tile
+    const u32 n0 = uniform(nx.x), n1 = uniform(nx.y), t63 = readlane(top, 63);
+    const u32 pn = pos + kTile;
+    const u32 nvn = pn < U ? ((U - pn) < 8u ? (U - pn) : 8u) : 0u;
+    const u32 B8 = (nz4(n0 ^ ((n0 << 8) | (t63 >> 24))) | (nz4(n1 ^ alignbyte(n1, n0, 3)) << 4) | ~lowmask(nvn)) & 0xFFu;
+    const u32 B24 = B | ((from_next_lane(B, B8) & 0xFFu) << 16);
 
-    // run phase carried across lanes: lane function q_in -> q_out
-    const uint32_t fcode = B ? 16u + mod9(15u - (31u - (uint32_t)__builtin_clz(B))) : 7u;  // (q+16)%9 == (q+7)%9
-    const uint32_t incl = wave_scan_incl(fcode, 0u, OpPhase9());
-    const uint32_t excl = from_prev_lane(incl, 0u);
-    const uint32_t qin = apply9(excl, st.q);
+    // run start of byte p0-1: max-scan of the last boundary position per lane
+    const u32 lbp = B ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
+    const u32 incl = wave_scan_incl(lbp, 0u, OpMax());
+    const u32 pm = from_prev_lane(incl, 0u);
+    const u32 rsl = pm > st.rs ? pm : st.rs;
+    const u32 qin = mod9(p0 - 1u - rsl);   // run phase of byte p0-1 (unused when p0 starts a run)
 
-    // token starts: run starts, run start + 9, and the continuation of the run entering the lane
-    const uint32_t f1 = B ? (uint32_t)__builtin_ctz(B) : 16u;
-    uint32_t t8 = B | (B << 1);
+    // token starts: run starts, 9 past a run start, and the continuation of the run entering
+    const u32 f1 = (u32)__builtin_ctz(B | 0x10000u);
+    u32 t8 = B | (B << 1);
     t8 |= t8 << 2;
     t8 |= t8 << 4;
     t8 |= B << 8;
-    const uint32_t j0 = 8u - qin;
-    const uint32_t pre = ((1u << j0) | (1u << (j0 + 9u))) & lowmask(f1);
-    const uint32_t T = (B | ((B << 9) & ~t8) | pre) & validm;
-    const uint32_t P = T & ~(B24 >> 1);  // 3-byte tokens (run continues past the start)
+    const u32 pre = (0x201u << (8u - qin)) & lowmask(f1);
+    const u32 T = (B | ((B << 9) & ~t8) | pre) & validm;
+    const u32 P = T & ~(B24 >> 1);   // 3-byte tokens: the run continues past the start
 
-    const uint32_t nout = (uint32_t)__builtin_popcount(T) + 2u * (uint32_t)__builtin_popcount(P);
-    const uint32_t oincl = wave_scan_incl(nout, 0u, OpAdd());
-    const uint32_t ttot = readlane(oincl, 63);
-    uint32_t o = (uint32_t)st.out_pos + (oincl - nout);   // ring index: low bits suffice
+    const u32 nout = bcnt(P, bcnt(P, bcnt(T, 0u)));
+    const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, 63);
+    const u32 rel0 = st.out_pos - st.flushed;   // 0..15: bytes of the partial chunk at stage[0..)
 
+    // pass 1: every position writes its byte.  A start writes at its token's offset; a
+    // non-start (inside a 3-byte token) writes the same byte at offset-2 of the NEXT token,
+    // which is its own token's second byte (a redundant, identical write) — so no position
+    // needs a branch or a dummy slot.
+    // Positions past U address like starts: they land at the tile's output end, never stored.
+    u32 o = rel0 + oincl - nout;
+    uint8_t* sb = stage + kEncGuard - 2;
+    const u32 TI = T | (~validm & 0xFFFFu);
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-        if (T & (1u << j)) {
-            const uint32_t x = byte_of(w, j);
-            ring[swz(o & (kEncRing - 1))] = (uint8_t)x;
-            if (P & (1u << j)) {
-                const uint32_t rem = (uint32_t)__builtin_ctz((B24 >> (j + 1)) | 0x100u) + 1u;  // min(9, run left)
-                ring[swz((o + 1) & (kEncRing - 1))] = (uint8_t)x;
-                ring[swz((o + 2) & (kEncRing - 1))] = (uint8_t)('0' + rem);
-                o += 3;
-            } else {
-                o += 1;
-            }
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 tb = bfe(T, j, 1), pb = bfe(P, j, 1);
+        sb[o + 2u * bfe(TI, j, 1)] = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
+        o += tb + 2u * pb;
+    }
+    // pass 2: second byte and count digit of each 3-byte token, written from the token's own
+    // tile (its second input byte may sit in the next tile, after this tile's flush)
+    u32 prem = P;
+    while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
+        if (prem) {
+            const u32 j = (u32)__builtin_ctz(prem);
+            prem &= prem - 1u;
+            const u32 mj = lowmask(j);
+            const u32 oj = rel0 + oincl - nout + bcnt(T & mj, 0u) + 2u * bcnt(P & mj, 0u);
+            const u32 rem = (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u) + 1u;   // min(9, run left)
+            const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
+            stage[kEncGuard + oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
+            stage[kEncGuard + oj + 2u] = (uint8_t)('0' + rem);
         }
     }
     wave_lds_sync();
 
-    // store every completed 16-byte chunk
-    const uint64_t newpos = st.out_pos + ttot;
-    const uint64_t c_hi = newpos >> 4;
-    for (uint64_t c0 = st.flushed >> 4; c0 < c_hi; c0 += kWave) {
-        const uint64_t c = c0 + lane;
-        if (c < c_hi) {
-            const uint32_t a = (uint32_t)(c * 16u) & (kEncRing - 1);
-            const uint32_t s = (a >> 7) & 7u;
-            uint4 v = *reinterpret_cast<const uint4*>(ring + (a ^ ((s & 4u) << 2)));
-            v = perm4(v, s & 3u);
-            *reinterpret_cast<uint4*>(dst + c * 16u) = v;
-        }
+    // store the completed 16-byte chunks, then move the partial chunk to the staging base
+    const u32 newrel = rel0 + ttot;
+    const u32 nfl = newrel >> 4;
+    const u32 rounds = (nfl + kWave - 1u) / kWave;
+    for (u32 k = 0; k < rounds; ++k) {
+        const u32 c = k * kWave + lane;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + kEncGuard + 16u * c);
+        vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, v);
+    }
+    if (nfl && lane == 0) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + kEncGuard + 16u * nfl);
+        *reinterpret_cast<u32x4*>(stage + kEncGuard) = v;
     }
     wave_lds_sync();
-    st.flushed = c_hi << 4;
-    st.out_pos = newpos;
-    st.prev_byte = last63;
-    st.q = apply9(readlane(incl, 63), st.q);
+    st.flushed += 16u * nfl;
+    st.out_pos += ttot;
+    st.prev_top = t63;
+    const u32 i63 = readlane(incl, 63);
+    st.rs = i63 > st.rs ? i63 : st.rs;
+    return rounds;
 }
 
 __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
@@ -226,40 +313,36 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_off,
                                                         uint64_t* __restrict__ out_len,
                                                         uint32_t* __restrict__ status, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWavesPerBlock * kEncRing];
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wid = uniform(threadIdx.x / kWave);
-    uint8_t* ring = ring_all + wid * kEncRing;
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 3 * kTile];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kWavesPerBlock * (kEncRing + kEncGuard)];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    uint8_t* stage = stage_all + wid * (kEncRing + kEncGuard);
+    const uint8_t* slots = slots_all + wid * 3 * kTile;
+    const u32 nw = gridDim.x * kWavesPerBlock;
 
-    for (uint32_t b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
-        const uint64_t U = in_len[b];
+    for (u32 b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
+        const uint64_t U64 = in_len[b];
         const uint8_t* src = in + in_off[b];
         uint8_t* dst = out + out_off[b];
-        if (((uintptr_t)src | (uintptr_t)dst) & 15u) {
+        u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+        if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+        if (bad) {
             if (lane == 0) {
                 out_len[b] = 0;
-                if (status) status[b] = RLE_STATUS_MISALIGNED;
+                if (status) status[b] = bad;
             }
             continue;
         }
-        EncState st{0, 0, 0, 0};
-        const uint64_t ntiles = (U + kTile - 1) / kTile;
-        uint4 cur = load_chunk(src, U, 16u * lane);
-        uint4 nxt = load_chunk(src, U, kTile + 16u * lane);
-        for (uint64_t t = 0; t < ntiles; ++t) {
-            const uint64_t pos = t * kTile;
-            const uint4 nn = load_chunk(src, U, pos + 2 * kTile + 16u * lane);
-            enc_tile(cur, nxt, pos, U, lane, ring, dst, st);
-            cur = nxt;
-            nxt = nn;
-        }
-        // the final partial chunk (< 16 bytes): byte stores so no byte past C is touched
-        const uint32_t rest = (uint32_t)(st.out_pos - st.flushed);
-        if (lane < rest) {
-            const uint32_t a = (uint32_t)(st.flushed + lane) & (kEncRing - 1);
-            dst[st.flushed + lane] = ring[swz(a)];
-        }
+        const u32 U = (u32)U64;
+        const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+        const u32x4 rso = make_rsrc(dst, U + U / 2u);
+        EncState st{0u, 0u, 0u, 0u};
+        walk_tiles(rsi, (U + kTile - 1u) / kTile, lane, slots, [&](u32 t, const uint8_t* cs, const uint8_t* ns) {
+            return enc_tile(cs, ns, t * kTile, U, lane, stage, rso, st);
+        });
+        // the final partial chunk (< 16 bytes): byte stores, nothing past C is touched
+        if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[kEncGuard + lane];
         if (lane == 0) {
             out_len[b] = st.out_pos;
             if (status) status[b] = RLE_STATUS_OK;
@@ -270,192 +353,195 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
 
 // ================================================================ DECODE
 // Token-phase table: for an 8-bit mask e of "byte j equals byte j+1" and entry offset d (the
-// first token start in the group), entry[e] bits 10d..10d+7 = token starts, 10d+8..9 = exit offset.
-__device__ __forceinline__ uint32_t dec_table_entry(uint32_t e) {
-    uint32_t ent = 0;
-    for (uint32_t d = 0; d < 3; ++d) {
-        uint32_t s = d, m = 0;
+// first token start in the group, 0..2): .x byte d = token-start mask, .y byte d = offset of the
+// first start past the group (.y byte 3 = 3, so .y is a v_perm selector).
+__device__ __forceinline__ uint2 dec_table_entry(u32 e) {
+    u32 masks = 0, exits = 3u << 24;
+    for (u32 d = 0; d < 3; ++d) {
+        u32 s = d, m = 0;
         while (s < 8) {
             m |= 1u << s;
             s += ((e >> s) & 1u) ? 3u : 1u;
         }
-        ent |= (m | ((s - 8u) << 8)) << (10u * d);
+        masks |= m << (8u * d);
+        exits |= (s - 8u) << (8u * d);
     }
-    return ent;
+    return make_uint2(masks, exits);
 }
 
 struct DecState {
-    uint64_t out_pos;   // decoded bytes produced so far
-    uint64_t flushed;   // decoded bytes already stored (multiple of 16)
-    uint32_t d;         // offset of the first token start in the current tile (0..2)
-    uint32_t fillc;     // 0x100|byte of the last stored position (hole-fill carry)
-    uint32_t tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
-    uint32_t serial;    // 1 -> stream needs the exact serial path
+    u32 out_pos;   // decoded bytes produced so far
+    u32 flushed;   // decoded bytes already stored (multiple of 16); staging base
+    u32 d;         // offset of the first token start in the current tile (0..2)
+    u32 fillc;     // 0x100|byte of the last stored position (run continuation carry)
+    u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
+    u32 serial;    // 1 -> stream needs the exact serial path
 };
 
-// Flush decoded chunks [c_lo, c_hi) from the hole-encoded u16 ring: positions hold 0x100|byte at
-// token starts and 0 elsewhere; each run is filled forward from its start.  Positions >= `total`
-// take `tailv` (0, or the unbounded final token's byte).  Chunks past U are never touched; the
-// chunk holding U is written byte-wise.
-__device__ __forceinline__ void dec_flush(uint64_t c_lo, uint64_t c_hi, uint64_t total, uint64_t U,
-                                          uint32_t tailv, uint32_t lane, uint16_t* ring, uint8_t* dst,
-                                          uint32_t& fillc) {
-    for (uint64_t c0 = c_lo; c0 < c_hi; c0 += kWave) {
-        const uint64_t c = c0 + lane;
-        const bool active = c < c_hi;
-        const bool in_ring = active && (c * 16u) < total;
-        uint32_t L[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        const uint32_t a = (uint32_t)(c * 32u) & (2u * kDecRing - 1u);  // byte address of the chunk
-        const uint32_t s = (a >> 7) & 7u;
-        if (in_ring) {
-            const uint4 v0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ring) + a);
-            const uint4 v1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ring) + a + 16u);
-            L[0] = v0.x; L[1] = v0.y; L[2] = v0.z; L[3] = v0.w;
-            L[4] = v1.x; L[5] = v1.y; L[6] = v1.z; L[7] = v1.w;
-            // undo the swizzle: logical dword k lives at physical k ^ s
-            cswap(L[0], L[1], s & 1u); cswap(L[2], L[3], s & 1u); cswap(L[4], L[5], s & 1u); cswap(L[6], L[7], s & 1u);
-            cswap(L[0], L[2], s & 2u); cswap(L[1], L[3], s & 2u); cswap(L[4], L[6], s & 2u); cswap(L[5], L[7], s & 2u);
-            cswap(L[0], L[4], s & 4u); cswap(L[1], L[5], s & 4u); cswap(L[2], L[6], s & 4u); cswap(L[3], L[7], s & 4u);
+// Store chunks [0, nch) (relative to st.flushed); chunks < nstaged are read from staging, the
+// rest hold no token start.  Staging holds 0x100|byte at token starts and 0 elsewhere; each
+// run is filled forward from its start; positions >= `valid` take `tailv`.  Read chunks are
+// re-zeroed.  Returns the number of store instructions issued.
+__device__ __forceinline__ u32 dec_flush(u32 nch, u32 nstaged, u32 valid, u32 tailv, u32 lane, uint16_t* stage,
+                                         u32x4 rso, u32 flushed, u32& fillc) {
+    const u32 rounds = (nch + kWave - 1u) / kWave;
+    for (u32 k = 0; k < rounds; ++k) {
+        const u32 c = k * kWave + lane;
+        const bool active = c < nch;
+        const bool staged = active && c < nstaged;
+        u32x4 v0 = u32x4{0u, 0u, 0u, 0u}, v1 = u32x4{0u, 0u, 0u, 0u};
+        if (staged) {
+            v0 = *reinterpret_cast<const u32x4*>(stage + 16u * c);
+            v1 = *reinterpret_cast<const u32x4*>(stage + 16u * c + 8u);
         }
-        uint32_t h[16];
+        const u32 L[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        u32 f[16];
+        u32 cur = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            h[2 * k] = L[k] & 0xFFFFu;
-            h[2 * k + 1] = L[k] >> 16;
+        for (u32 j = 0; j < 16; ++j) {
+            const u32 h = (j & 1u) ? (L[j >> 1] >> 16) : (L[j >> 1] & 0xFFFFu);
+            cur = h ? h : cur;
+            f[j] = cur;
         }
-        uint32_t lastp = 0;
+        const u32 lastp = active ? cur : 0u;
+        const u32 incl = wave_scan_incl(lastp, 0u, OpLatest());
+        const u32 before = from_prev_lane(incl, 0u);
+        const u32 carry = before ? before : fillc;
+        u32 ob[4] = {0u, 0u, 0u, 0u};
+        const u32 pbase = 16u * c;
 #pragma unroll
-        for (uint32_t j = 0; j < 16; ++j) lastp = h[j] ? h[j] : lastp;
-        const uint32_t incl = wave_scan_incl(lastp, 0u, OpLatest());
-        const uint32_t before = from_prev_lane(incl, 0u);
-        uint32_t cur = before ? before : fillc;
-        uint32_t ob[4] = {0, 0, 0, 0};
-        const uint64_t pbase = c * 16u;
-#pragma unroll
-        for (uint32_t j = 0; j < 16; ++j) {
-            cur = h[j] ? h[j] : cur;
-            const uint32_t byte = (pbase + j) < total ? (cur & 0xFFu) : tailv;
-            ob[j >> 2] |= byte << (8u * (j & 3u));
+        for (u32 j = 0; j < 16; ++j) {
+            const u32 val = (pbase + j) < valid ? ((f[j] ? f[j] : carry) & 0xFFu) : tailv;
+            ob[j >> 2] |= val << (8u * (j & 3u));
         }
-        if (active) {
-            if (pbase + 16u <= U) {
-                *reinterpret_cast<uint4*>(dst + pbase) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-            } else {
-                for (uint32_t j = 0; j < 16u && pbase + j < U; ++j) dst[pbase + j] = (uint8_t)(ob[j >> 2] >> (8u * (j & 3u)));
-            }
-            if (in_ring) {
-                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ring) + a) = make_uint4(0u, 0u, 0u, 0u);
-                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ring) + a + 16u) = make_uint4(0u, 0u, 0u, 0u);
-            }
+        u32x4 o;
+        o.x = ob[0]; o.y = ob[1]; o.z = ob[2]; o.w = ob[3];
+        vstore(rso, active ? flushed + pbase : kOOB, o);
+        if (staged) {
+            *reinterpret_cast<u32x4*>(stage + 16u * c) = u32x4{0u, 0u, 0u, 0u};
+            *reinterpret_cast<u32x4*>(stage + 16u * c + 8u) = u32x4{0u, 0u, 0u, 0u};
         }
-        const uint64_t lastlane = (c_hi - 1u - c0) < (kWave - 1u) ? (c_hi - 1u - c0) : (kWave - 1u);
-        fillc = readlane(cur, (uint32_t)lastlane);
+        const u32 lastlane = (nch - 1u - k * kWave) < (kWave - 1u) ? (nch - 1u - k * kWave) : (kWave - 1u);
+        const u32 lv = readlane(f[15] ? f[15] : carry, lastlane);
+        fillc = lv;
         wave_lds_sync();
     }
+    return rounds;
 }
 
-__device__ __forceinline__ void dec_tile(uint4 cur, const uint4 nxt, uint64_t pos, uint64_t C, uint64_t U,
-                                         uint32_t lane, const uint32_t* tbl, uint16_t* ring, uint8_t* dst,
-                                         DecState& st) {
-    const uint64_t p0 = pos + 16u * lane;
-    const uint32_t nl = p0 >= C ? 0u : (uint32_t)((C - p0) < 16u ? (C - p0) : 16u);
-    const uint32_t validm = lowmask(nl);
-    // bytes at index >= C read as the zero padding of the stored stream
-    uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const uint8_t* nslot, u32 pos, u32 C, u32 U,
+                                        u32 lane, const uint2* tbl, uint16_t* stage, uint16_t* trash, u32x4 rso,
+                                        DecState& st) {
+    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    const u32 p0 = pos + 16u * lane;
+    const u32 left = p0 < C ? C - p0 : 0u;
+    const u32 nl = left < 16u ? left : 16u;
+    const u32 validm = lowmask(nl);
+    u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+    if (pos + kTile > C) {   // last tile: bytes at index >= C read as the stream's zero padding
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t nb = nl > 4u * k ? (nl - 4u * k < 4u ? nl - 4u * k : 4u) : 0u;
-        w[k] &= lowmask(8u * nb);
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 nb = nl > 4u * k ? (nl - 4u * k < 4u ? nl - 4u * k : 4u) : 0u;
+            w[k] &= lowmask(8u * nb);
+        }
     }
     // 2-byte lookahead: next lane's first bytes; lane 63 reads the next tile
-    const uint64_t pn = pos + kTile;
-    const uint32_t nvn = pn >= C ? 0u : (uint32_t)((C - pn) < 2u ? (C - pn) : 2u);
-    const uint32_t nx = readlane(nxt.x, 0) & lowmask(8u * nvn);
-    const uint32_t la = from_next_lane(w[0] & 0xFFFFu, nx) & 0xFFFFu;
+    const u32 pn = pos + kTile;
+    const u32 nvn = pn < C ? ((C - pn) < 2u ? (C - pn) : 2u) : 0u;
+    const u32 nx = uniform(*reinterpret_cast<const u32*>(nslot)) & lowmask(8u * nvn);
+    const u32 la = from_next_lane(w[0] & 0xFFFFu, nx) & 0xFFFFu;
 
     // E bit j <=> y[j] == y[j+1]  (a token starting at j is then 3 bytes long)
-    const uint32_t NE = nz4(w[0] ^ ((w[0] >> 8) | (w[1] << 24))) | (nz4(w[1] ^ ((w[1] >> 8) | (w[2] << 24))) << 4) |
-                        (nz4(w[2] ^ ((w[2] >> 8) | (w[3] << 24))) << 8) | (nz4(w[3] ^ ((w[3] >> 8) | (la << 24))) << 12);
-    const uint32_t E = ~NE & 0xFFFFu;
-    const uint32_t ta = tbl[E & 0xFFu], tb = tbl[E >> 8];
-    uint32_t map = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 3; ++d) {
-        const uint32_t mid = (ta >> (10u * d + 8u)) & 3u;
-        map |= ((tb >> (10u * mid + 8u)) & 3u) << (2u * d);
-    }
-    const uint32_t incl = wave_scan_incl(map, kMap3Id, OpMap3());
-    const uint32_t excl = from_prev_lane(incl, kMap3Id);
-    const uint32_t dl = (excl >> (2u * st.d)) & 3u;
-    const uint32_t mid = (ta >> (10u * dl + 8u)) & 3u;
-    const uint32_t S = (((ta >> (10u * dl)) & 0xFFu) | (((tb >> (10u * mid)) & 0xFFu) << 8)) & validm;
-    const uint32_t P = S & E;
+    const u32 NE = nz4(w[0] ^ alignbyte(w[1], w[0], 1)) | (nz4(w[1] ^ alignbyte(w[2], w[1], 1)) << 4) |
+                   (nz4(w[2] ^ alignbyte(w[3], w[2], 1)) << 8) | (nz4(w[3] ^ alignbyte(la, w[3], 1)) << 12);
+    const u32 E = ~NE & 0xFFFFu;
+    const uint2 ta = tbl[E & 0xFFu], tb = tbl[E >> 8];
+    const u32 map = __builtin_amdgcn_perm(tb.y, tb.y, ta.y);
+    const u32 incl = wave_scan_incl(map, kMapId, OpMap());
+    const u32 excl = from_prev_lane(incl, kMapId);
+    const u32 dl = bfe(excl, 8u * st.d, 8);
+    const u32 mid = bfe(ta.y, 8u * dl, 8);
+    const u32 S = (bfe(ta.x, 8u * dl, 8) | (bfe(tb.x, 8u * mid, 8) << 8)) & validm;
+    const u32 P = S & E;
 
-    // token lengths: count = (signed char)digit - '0'; <=1 -> 1 byte; 2..9 -> count;
-    // >9 -> serial path; <0 (unbounded, fills to U) -> allowed only as the final token
-    uint32_t len[16];
-    bool serial = false, inf = false;
-    uint32_t infval = 0;
+    // token lengths: digit d (byte j+2) in '1'..'9' -> d-'0'; digits in the zero padding mark
+    // the stream's final token (unbounded count: fills to U); anything else -> serial path
+    const u32 left18 = left < 18u ? left : 18u;
+    const u32 v18 = lowmask(left18);
+    const u32 MP = P & (v18 >> 2);
+    const u32 PF = P & ~(v18 >> 2);
+    const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
+                       alignbyte(la, w[3], 2)};
+    u32 dm1[4], extra = 0, badb = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-        len[j] = 1u;
-        if (P & (1u << j)) {
-            const uint32_t db = (j + 2u) < 16u ? byte_of(w, j + 2u) : ((la >> (8u * (j + 2u - 16u))) & 0xFFu);
-            const int v = (int)(int8_t)db - 48;
-            if (v > 9) serial = true;
-            else if (v >= 2) len[j] = (uint32_t)v;
-            else if (v < 0) {
-                inf = true;
-                infval = 0x100u | byte_of(w, j);
-                if (p0 + j + 3u < C) serial = true;   // not the final token
-            }
-        }
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 mpb = nib_to_bytes(bfe(MP, 4u * k, 4));
+        const u32 dor = dg[k] | 0x80808080u;
+        const u32 lo = dor - 0x31313131u, hi = dor - 0x3A3A3A3Au;
+        dm1[k] = lo & 0x7F7F7F7Fu;   // d - '1' for d in ['1', 0x80)
+        extra = __builtin_amdgcn_udot4(dm1[k], mpb, extra, false);
+        badb |= (~lo | hi | dg[k]) & (mpb << 7);
     }
-    uint32_t nout = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) nout += (S & (1u << j)) ? len[j] : 0u;
-    const uint32_t oincl = wave_scan_incl(nout, 0u, OpAdd());
-    const uint32_t ttot = readlane(oincl, 63);
-    const uint64_t newpos = st.out_pos + ttot;
-    if (__any(serial) || newpos > U) {
+    const u32 nout = bcnt(S, extra);
+    const bool serial_lane = badb != 0u || (PF & (v18 >> 1)) != 0u;
+    const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, 63);
+    if (__builtin_amdgcn_ballot_w64(serial_lane) || st.out_pos + ttot > U) {
         st.serial = 1;
-        return;
+        return ~0u;
     }
-    const unsigned long long infb = __ballot(inf);
-    if (infb) st.tail = readlane(infval, (uint32_t)__builtin_ctzll(infb));
+    const uint64_t pfb = __builtin_amdgcn_ballot_w64(PF != 0u);
+    if (pfb) {   // the final token's byte extends to U
+        const u32 jf = (u32)__builtin_ctz(PF | 0x10000u) & 15u;
+        const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
+        st.tail = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+    }
 
-    uint32_t o = (uint32_t)st.out_pos + (oincl - nout);
+    // scatter 0x100|byte at each token start's decoded position; non-starts write a private slot
+    const u32 rel0 = st.out_pos - st.flushed;
+    u32 o = rel0 + oincl - nout;
+    uint16_t* tr = trash + lane;
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-        if (S & (1u << j)) {
-            ring[swz(2u * (o & (kDecRing - 1))) >> 1] = (uint16_t)(0x100u | byte_of(w, j));
-            o += len[j];
-        }
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 sbit = bfe(S, j, 1);
+        uint16_t* p = sbit ? stage + o : tr;
+        *p = (uint16_t)(0x100u | bfe(w[j >> 2], 8u * (j & 3u), 8));
+        o += sbit + bfe(MP, j, 1) * bfe(dm1[j >> 2], 8u * (j & 3u), 8);
     }
     wave_lds_sync();
-    const uint64_t c_hi = newpos >> 4;
-    dec_flush(st.flushed >> 4, c_hi, newpos, U, 0u, lane, ring, dst, st.fillc);
-    st.flushed = c_hi << 4;
-    st.out_pos = newpos;
-    st.d = (readlane(incl, 63) >> (2u * st.d)) & 3u;
+
+    const u32 newrel = rel0 + ttot;
+    const u32 nfl = newrel >> 4;
+    const u32 rounds = dec_flush(nfl, nfl, newrel, 0u, lane, stage, rso, st.flushed, st.fillc);
+    if (nfl) {   // move the partial chunk to the staging base
+        if (lane < 2u) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16u * nfl + 8u * lane);
+            *reinterpret_cast<u32x4*>(stage + 8u * lane) = v;
+            *reinterpret_cast<u32x4*>(stage + 16u * nfl + 8u * lane) = u32x4{0u, 0u, 0u, 0u};
+        }
+        wave_lds_sync();
+    }
+    st.flushed += 16u * nfl;
+    st.out_pos += ttot;
+    st.d = bfe(readlane(incl, 63), 8u * st.d, 8);
+    return rounds;
 }
 
 // Exact serial decode (src/rleCompression.c:47-62 semantics, writes capped at cap) for the
-// streams the tiled path declines: counts > 9, unbounded counts before the last token, or
-// streams that decode to more than U bytes.  One lane; such streams never come from the encoder.
-__device__ uint32_t dec_serial(const uint8_t* src, uint64_t C, uint64_t U, uint64_t cap, uint8_t* dst,
-                               uint32_t lane, uint16_t* ring) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t k = lane; k < kDecRing * 2u / 16u; k += kWave)
-        reinterpret_cast<uint4*>(ring)[k] = make_uint4(0u, 0u, 0u, 0u);
+// streams the tiled path declines: counts outside '1'..'9', unbounded counts before the last
+// token, or streams that decode to more than U bytes.  One lane; the encoder never emits these.
+__device__ u32 dec_serial(const uint8_t* src, u32 C, u32 U, uint64_t cap, uint8_t* dst, u32 lane,
+                          uint16_t* stage) {
+    for (u32 k = lane; k < kDecRing * 2u / 16u; k += kWave)
+        reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     for (uint64_t c = lane; c * 16u < cap; c += kWave) {
-        if (c * 16u + 16u <= cap) *reinterpret_cast<uint4*>(dst + c * 16u) = make_uint4(0u, 0u, 0u, 0u);
+        if (c * 16u + 16u <= cap) *reinterpret_cast<u32x4*>(dst + c * 16u) = u32x4{0u, 0u, 0u, 0u};
         else
             for (uint64_t p = c * 16u; p < cap; ++p) dst[p] = 0;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_drain();
     wave_lds_sync();
-    uint32_t st = RLE_STATUS_SERIAL;
+    u32 st = RLE_STATUS_SERIAL;
     if (lane == 0) {
         uint64_t o = 0, j = 0;
         while (j < C) {
@@ -464,20 +550,20 @@ __device__ uint32_t dec_serial(const uint8_t* src, uint64_t C, uint64_t U, uint6
             dst[o++] = v;
             const uint8_t n1 = (j + 1 < C) ? src[j + 1] : (uint8_t)0;
             if (v == n1) {
-                const uint8_t dg = (j + 2 < C) ? src[j + 2] : (uint8_t)0;
-                const int occ = (int)(int8_t)dg - 48;
-                const uint64_t extra = occ < 0 ? ~0ull : (occ >= 2 ? (uint64_t)(occ - 1) : 0ull);
+                const uint8_t dgt = (j + 2 < C) ? src[j + 2] : (uint8_t)0;
+                const int occ = (int)(int8_t)dgt - 48;
+                const uint64_t ex = occ < 0 ? ~0ull : (occ >= 2 ? (uint64_t)(occ - 1) : 0ull);
                 const uint64_t room = o < U ? U - o : 0;
-                const uint64_t k = extra < room ? extra : room;
-                for (uint64_t i = 0; i < k; ++i) dst[o + i] = v;
-                o += k;
+                const uint64_t kk = ex < room ? ex : room;
+                for (uint64_t i = 0; i < kk; ++i) dst[o + i] = v;
+                o += kk;
                 j += 3;
             } else {
                 j += 1;
             }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_drain();
     return readlane(st, 0);
 }
 
@@ -489,45 +575,64 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_len,
                                                         const uint64_t* __restrict__ out_cap,
                                                         uint32_t* __restrict__ status, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint16_t ring_all[kWavesPerBlock * kDecRing];
-    __shared__ uint32_t tbl[256];
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 3 * kTile];
+    __shared__ __attribute__((aligned(16))) uint16_t stage_all[kWavesPerBlock * kDecRing];
+    __shared__ __attribute__((aligned(16))) uint16_t trash_all[kWavesPerBlock * kWave];
+    __shared__ uint2 tbl[256];
     tbl[threadIdx.x] = dec_table_entry(threadIdx.x);
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wid = uniform(threadIdx.x / kWave);
-    uint16_t* ring = ring_all + wid * kDecRing;
-    for (uint32_t k = lane; k < kDecRing * 2u / 16u; k += kWave)
-        reinterpret_cast<uint4*>(ring)[k] = make_uint4(0u, 0u, 0u, 0u);
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    uint16_t* stage = stage_all + wid * kDecRing;
+    uint16_t* trash = trash_all + wid * kWave;
+    const uint8_t* slots = slots_all + wid * 3 * kTile;
+    for (u32 k = lane; k < kDecRing * 2u / 16u; k += kWave)
+        reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    const u32 nw = gridDim.x * kWavesPerBlock;
 
-    for (uint32_t b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
-        const uint64_t C = in_len[b];
-        const uint64_t U = out_len[b];
-        const uint64_t cap = out_cap ? out_cap[b] : U;
+    for (u32 b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
+        const uint64_t C64 = in_len[b];
+        const uint64_t U64 = out_len[b];
+        const uint64_t cap = out_cap ? out_cap[b] : U64;
         const uint8_t* src = in + in_off[b];
         uint8_t* dst = out + out_off[b];
-        if ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U) {
-            if (lane == 0 && status) status[b] = RLE_STATUS_MISALIGNED;
+        u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
+        if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+        if (bad) {
+            if (lane == 0 && status) status[b] = bad;
             continue;
         }
-        DecState st{0, 0, 0, 0, 0, 0};
-        const uint64_t ntiles = (C + kTile - 1) / kTile;
-        uint4 cur = load_chunk(src, C, 16u * lane);
-        uint4 nxt = load_chunk(src, C, kTile + 16u * lane);
-        for (uint64_t t = 0; t < ntiles; ++t) {
-            const uint64_t pos = t * kTile;
-            const uint4 nn = load_chunk(src, C, pos + 2 * kTile + 16u * lane);
-            dec_tile(cur, nxt, pos, C, U, lane, tbl, ring, dst, st);
-            if (st.serial) break;
-            cur = nxt;
-            nxt = nn;
-        }
-        uint32_t stat = RLE_STATUS_OK;
+        const u32 C = (u32)C64, U = (u32)U64;
+        const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+        const u32x4 rso = make_rsrc(dst, U);
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u};
+        walk_tiles(rsi, (C + kTile - 1u) / kTile, lane, slots, [&](u32 t, const uint8_t* cs, const uint8_t* ns) {
+            return dec_tile(cs, ns, t * kTile, C, U, lane, tbl, stage, trash, rso, st);
+        });
+        u32 stat = RLE_STATUS_OK;
         if (st.serial) {
-            stat = dec_serial(src, C, U, cap, dst, lane, ring);
+            stat = dec_serial(src, C, U, cap, dst, lane, stage);
         } else {
-            // remaining positions: the partial chunk still in the ring, then [total, U)
-            dec_flush(st.flushed >> 4, (U + 15u) >> 4, st.out_pos, U, st.tail & 0xFFu, lane, ring, dst, st.fillc);
+            // the partial chunk still staged, then [out_pos, U): zeros, or the final
+            // unbounded token's byte; the chunk holding U is written byte by byte
+            const u32 rel = st.out_pos - st.flushed;   // staged positions (chunk 0 only)
+            const u32 span = U - st.flushed;
+            const u32 full = span >> 4, tailn = span & 15u;
+            const u32 tv = st.tail & 0xFFu;
+            dec_flush(full, 1u, rel, tv, lane, stage, rso, st.flushed, st.fillc);
+            if (tailn) {
+                u32 v = st.fillc;
+                if (full == 0u)
+                    for (u32 j = 0; j <= lane && j < 16u; ++j) {
+                        const u32 hj = stage[j];
+                        v = hj ? hj : v;
+                    }
+                const u32 p = 16u * full + lane;
+                if (lane < tailn) dst[st.flushed + p] = (uint8_t)(p < rel ? (v & 0xFFu) : tv);
+                wave_lds_sync();
+                if (full == 0u && lane < 2u) reinterpret_cast<u32x4*>(stage)[lane] = u32x4{0u, 0u, 0u, 0u};
+            }
+            vm_drain();
         }
         if (lane == 0 && status) status[b] = stat;
         wave_lds_sync();
@@ -591,7 +696,6 @@ __global__ void selftest_kernel(uint32_t* err) {
     uint32_t ref = 0;
     for (uint32_t l = 0; l <= lane; ++l) ref += v[l] & 0xFFFu;
     if (sum != ref) e |= 4;
-    // phase-9 composition against a lane-serial fold
     const uint32_t f = (x & 1u) ? 16u + (x >> 3) % 9u : (x >> 5) % 9u;
     const uint32_t sc = wave_scan_incl(f, 0u, OpPhase9());
     uint32_t rf = 0;
@@ -600,14 +704,21 @@ __global__ void selftest_kernel(uint32_t* err) {
         rf = OpPhase9()(rf, (y & 1u) ? 16u + (y >> 3) % 9u : (y >> 5) % 9u);
     }
     if (sc != rf) e |= 8;
-    const uint32_t m = ((x % 3u)) | (((x >> 4) % 3u) << 2) | (((x >> 8) % 3u) << 4);
-    const uint32_t sm = wave_scan_incl(m, kMap3Id, OpMap3());
-    uint32_t rm = kMap3Id;
+    const uint32_t m = 0x03000000u | (x % 3u) | (((x >> 4) % 3u) << 8) | (((x >> 8) % 3u) << 16);
+    const uint32_t sm = wave_scan_incl(m, kMapId, OpMap());
+    uint32_t rm = kMapId;
     for (uint32_t l = 0; l <= lane; ++l) {
         const uint32_t y = v[l];
-        rm = OpMap3()(rm, ((y % 3u)) | (((y >> 4) % 3u) << 2) | (((y >> 8) % 3u) << 4));
+        const uint32_t my = 0x03000000u | (y % 3u) | (((y >> 4) % 3u) << 8) | (((y >> 8) % 3u) << 16);
+        rm = OpMap()(rm, my);
     }
     if (sm != rm) e |= 16;
+    const uint32_t mx = wave_scan_incl(x & 0xFFFFu, 0u, OpMax());
+    uint32_t rx = 0;
+    for (uint32_t l = 0; l <= lane; ++l) rx = (v[l] & 0xFFFFu) > rx ? (v[l] & 0xFFFFu) : rx;
+    if (mx != rx) e |= 32;
+    if (nz4(0x00FF0100u) != 0x6u || nz4(0x80000001u) != 0x9u || nz4(0u) != 0u || nz4(0xFFFFFFFFu) != 0xFu) e |= 64;
+    if (mod9(1000000007u) != 1000000007u % 9u || mod9(0xFFFFFFFFu) != 0xFFFFFFFFu % 9u) e |= 128;
     if (e) atomicOr(err, e);
 }
 
@@ -672,4 +783,4 @@ extern "C" int rle_mi355x_device_count(void) {
     return n;
 }
 
-extern "C" const char* rle_mi355x_version(void) { return "rle_mi355x 0.1 (gfx950, wave-per-buffer tiled codec)"; }
+extern "C" const char* rle_mi355x_version(void) { return "rle_mi355x 0.2 (gfx950, wave-per-buffer tiled codec)"; }

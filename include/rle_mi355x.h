@@ -43,6 +43,7 @@ extern "C" {
 #define RLE_STATUS_OK          0u
 #define RLE_STATUS_OVERFLOW    1u      /* decode: stream writes past cap (reference: heap overflow); truncated */
 #define RLE_STATUS_MISALIGNED  2u      /* input or output slot not 16-byte aligned; buffer skipped */
+#define RLE_STATUS_TOOLARGE    4u      /* buffer larger than 0x7FFFFFF0 bytes (2 GiB); buffer skipped */
 #define RLE_STATUS_SERIAL      0x100u  /* info: stream decoded by the exact serial path (not encoder output) */
 
 /* Worst-case compressed size of U bytes (every run of length 2: 3 bytes per 2 input bytes). */
