@@ -30,10 +30,6 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 constexpr u32 kWave = 64;
 constexpr u32 kWavesPerBlock = 4;
 constexpr u32 kBlock = kWave * kWavesPerBlock;
-constexpr u32 kTile = 1024;       // input bytes per wave step (16 per lane)
-constexpr u32 kEncRing = 2048;    // encode staging bytes per wave (tile output <= 1538 + 15)
-constexpr u32 kEncGuard = 16;     // non-start positions may write 2 bytes before the tile base
-constexpr u32 kDecRing = 3120;    // decode staging positions (u16) per wave: <= 194 chunks + partial
 constexpr u32 kMaxBlocks = 8192;
 constexpr u32 kMaxBufferBytes = 0x7FFFFFF0u;   // per-buffer limit (32-bit in-buffer offsets)
 constexpr u32 kOOB = 0x80000000u;               // store offset dropped by the range check
@@ -155,84 +151,84 @@ __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v) {
         asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
         break;
 __device__ __forceinline__ void vm_wait(u32 n) {
-    switch (n < 12u ? n : 12u) {
-        RLE_VMW(0) RLE_VMW(1) RLE_VMW(2) RLE_VMW(3) RLE_VMW(4) RLE_VMW(5) RLE_VMW(6)
-        RLE_VMW(7) RLE_VMW(8) RLE_VMW(9) RLE_VMW(10) RLE_VMW(11) RLE_VMW(12)
+    switch (n < 8u ? n : 8u) {
+        RLE_VMW(0) RLE_VMW(1) RLE_VMW(2) RLE_VMW(3) RLE_VMW(4) RLE_VMW(5) RLE_VMW(6) RLE_VMW(7) RLE_VMW(8)
         default: break;
     }
 }
 #undef RLE_VMW
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Walk one buffer's tiles with loads three tiles deep into three LDS slots (1 KiB each),
-// rotating slots by unrolling.  step(t, cur, nxt) processes tile t from slot `cur` (nxt = slot
-// of tile t+1, its lookahead) and returns the number of store instructions it issued, or ~0u
-// to stop early.  The wait before a step counts those stores: they are younger than the load
-// it needs.
+// Tiles overlap: tile t is input [1008 t, 1008 t + 1024); lanes 0..62 own its first 1008 bytes
+// and lane 63 holds the next tile's first 16 bytes (the lookahead of lane 62).  Each tile is one
+// LDS-DMA into one of two slots, issued one tile ahead.  step(t, slot) processes tile t and
+// returns the store instructions it issued (or ~0u to stop); the wait before a step counts
+// them, because they are younger than the load it needs.
+constexpr u32 kOwnLanes = 63;
+constexpr u32 kTileStep = 16 * kOwnLanes;   // 1008
+constexpr u32 kSlot = 16 * kWave;           // 1024
 template <class Step>
 __device__ __forceinline__ void walk_tiles(u32x4 rs, u32 ntiles, u32 lane, const uint8_t* slots, Step step) {
     const u32 lo = 16u * lane;
     const uint8_t* s0 = slots;
-    const uint8_t* s1 = slots + kTile;
-    const uint8_t* s2 = slots + 2 * kTile;
-    const u32 l0 = uniform(lds_addr(s0)), l1 = l0 + kTile, l2 = l0 + 2 * kTile;
+    const uint8_t* s1 = slots + kSlot;
+    const u32 l0 = uniform(lds_addr(s0)), l1 = l0 + kSlot;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
     dma_tile(rs, lo, l0);
-    dma_tile(rs, kTile + lo, l1);
-    dma_tile(rs, 2 * kTile + lo, l2);
+    dma_tile(rs, kTileStep + lo, l1);
     u32 prev = 0;
-    for (u32 t = 0; t < ntiles; t += 3) {
+    for (u32 t = 0; t < ntiles; t += 2) {
         vm_wait(prev + 1);
-        prev = step(t, s0, s1);
+        prev = step(t, s0);
         if (prev == ~0u || t + 1 >= ntiles) break;
-        dma_tile(rs, (t + 3) * kTile + lo, l0);
+        dma_tile(rs, (t + 2) * kTileStep + lo, l0);
         vm_wait(prev + 1);
-        prev = step(t + 1, s1, s2);
-        if (prev == ~0u || t + 2 >= ntiles) break;
-        dma_tile(rs, (t + 4) * kTile + lo, l1);
-        vm_wait(prev + 1);
-        prev = step(t + 2, s2, s0);
+        prev = step(t + 1, s1);
         if (prev == ~0u) break;
-        dma_tile(rs, (t + 5) * kTile + lo, l2);
+        dma_tile(rs, (t + 3) * kTileStep + lo, l1);
     }
     vm_drain();
 }
+__device__ __forceinline__ u32 ntiles_for(u32 n) { return (n + kTileStep - 1u) / kTileStep; }
+
+// packed u16 max
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32 pkmax(u32 a, u32 b) {
+    return __builtin_bit_cast(u32, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+}
 
 // ================================================================ ENCODE
+// Staging (per wave): output position r of the tile (biased by 16: chunk 0 is a guard for the
+// back-writes of non-starts) lives at byte r.
+constexpr u32 kEncStage = 2048;   // >= 16 + 15 + 1512 + 2
+
 struct EncState {
     u32 out_pos;    // compressed bytes produced so far
-    u32 flushed;    // compressed bytes already stored (multiple of 16); staging base
+    u32 flushed;    // compressed bytes already stored (multiple of 16); staging chunk 1 = flushed
     u32 prev_top;   // input byte at tile_pos-1, in bits 24..31
     u32 rs;         // start position of the run holding input byte tile_pos-1
 };
 
-__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const uint8_t* nslot, u32 pos, u32 U, u32 lane,
-                                        uint8_t* stage, u32x4 rso, EncState& st) {
+__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, u32 pos, u32 U, u32 lane, uint8_t* stage, u32x4 rso,
+                                        EncState& st) {
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
-    const uint2 nx = *reinterpret_cast<const uint2*>(nslot);
     const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
     const u32 p0 = pos + 16u * lane;
-    const u32 nl = p0 < U ? ((U - p0) < 16u ? (U - p0) : 16u) : 0u;
-    const u32 validm = lowmask(nl);
+    const u32 left = p0 < U ? U - p0 : 0u;
+    const u32 nl = left < 16u ? left : 16u;
+    const u32 validm = lane < kOwnLanes ? lowmask(nl) : 0u;   // lane 63 only supplies lookahead
 
-    // run boundaries: bit j <=> x[p0+j] != x[p0+j-1] (or p0+j == 0); positions >= U count as
-    // boundaries (they end the last run)
+    // run boundaries: bit j <=> x[p0+j] != x[p0+j-1] (or p0+j == 0); positions >= U end runs
     const u32 top = w[3] & 0xFF000000u;
     const u32 ptop = from_prev_lane(top, st.prev_top);
     u32 B = nz4(w[0] ^ alignbyte(w[0], ptop, 3)) | (nz4(w[1] ^ alignbyte(w[1], w[0], 3)) << 4) |
             (nz4(w[2] ^ alignbyte(w[2], w[1], 3)) << 8) | (nz4(w[3] ^ alignbyte(w[3], w[2], 3)) << 12);
     B |= (p0 == 0u) ? 1u : 0u;
-    B |= ~validm & 0xFFFFu;
+    B |= ~lowmask(nl) & 0xFFFFu;
+    const u32 B24 = B | ((from_next_lane(B, 0xFFu) & 0xFFu) << 16);   // + next 8 bytes (repeat lookahead)
 
-    // boundaries of the next 8 bytes (repeat-count lookahead); lane 63 reads the next tile
-    const u32 n0 = uniform(nx.x), n1 = uniform(nx.y), t63 = readlane(top, 63);
-    const u32 pn = pos + kTile;
-    const u32 nvn = pn < U ? ((U - pn) < 8u ? (U - pn) : 8u) : 0u;
-    const u32 B8 = (nz4(n0 ^ ((n0 << 8) | (t63 >> 24))) | (nz4(n1 ^ alignbyte(n1, n0, 3)) << 4) | ~lowmask(nvn)) & 0xFFu;
-    const u32 B24 = B | ((from_next_lane(B, B8) & 0xFFu) << 16);
-
-    // run start of byte p0-1: max-scan of the last boundary position per lane
-    const u32 lbp = B ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
+    // run start of byte p0-1: max-scan of the last boundary position per owning lane
+    const u32 lbp = (B && lane < kOwnLanes) ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
     const u32 incl = wave_scan_incl(lbp, 0u, OpMax());
     const u32 pm = from_prev_lane(incl, 0u);
     const u32 rsl = pm > st.rs ? pm : st.rs;
@@ -251,21 +247,26 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const uint8_t* nsl
     const u32 nout = bcnt(P, bcnt(P, bcnt(T, 0u)));
     const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
     const u32 ttot = readlane(oincl, 63);
-    const u32 rel0 = st.out_pos - st.flushed;   // 0..15: bytes of the partial chunk at stage[0..)
+    const u32 rel0 = st.out_pos - st.flushed;   // 0..15: bytes of the partial chunk
 
-    // pass 1: every position writes its byte.  A start writes at its token's offset; a
+    // pass 1: every position writes its byte.  A start writes at its token's offset; a valid
     // non-start (inside a 3-byte token) writes the same byte at offset-2 of the NEXT token,
-    // which is its own token's second byte (a redundant, identical write) — so no position
-    // needs a branch or a dummy slot.
-    // Positions past U address like starts: they land at the tile's output end, never stored.
-    u32 o = rel0 + oincl - nout;
-    uint8_t* sb = stage + kEncGuard - 2;
-    const u32 TI = T | (~validm & 0xFFFFu);
+    // i.e. its own token's second byte (a redundant, identical write); positions past U write
+    // at the tile's output end, which is never stored.  Per-position weights (T + 2P) and
+    // back-offsets (2 for valid non-starts) are byte vectors.
+    const u32 NS = validm & ~T;
+    u32 W[4], D[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        W[k] = nib_to_bytes(bfe(T, 4u * k, 4)) + 2u * nib_to_bytes(bfe(P, 4u * k, 4));
+        D[k] = 2u * nib_to_bytes(bfe(NS, 4u * k, 4));
+    }
+    u32 o = lds_addr(stage) + 16u + rel0 + oincl - nout;   // LDS byte address of the lane's output
 #pragma unroll
     for (u32 j = 0; j < 16; ++j) {
-        const u32 tb = bfe(T, j, 1), pb = bfe(P, j, 1);
-        sb[o + 2u * bfe(TI, j, 1)] = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
-        o += tb + 2u * pb;
+        const u32 a = o - ((D[j >> 2] >> (8u * (j & 3u))) & 0xFFu);
+        *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
+        o += (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
     }
     // pass 2: second byte and count digit of each 3-byte token, written from the token's own
     // tile (its second input byte may sit in the next tile, after this tile's flush)
@@ -275,32 +276,33 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const uint8_t* nsl
             const u32 j = (u32)__builtin_ctz(prem);
             prem &= prem - 1u;
             const u32 mj = lowmask(j);
-            const u32 oj = rel0 + oincl - nout + bcnt(T & mj, 0u) + 2u * bcnt(P & mj, 0u);
+            const u32 oj = 16u + rel0 + oincl - nout + bcnt(T & mj, 0u) + 2u * bcnt(P & mj, 0u);
             const u32 rem = (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u) + 1u;   // min(9, run left)
             const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
-            stage[kEncGuard + oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
-            stage[kEncGuard + oj + 2u] = (uint8_t)('0' + rem);
+            stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
+            stage[oj + 2u] = (uint8_t)('0' + rem);
         }
     }
     wave_lds_sync();
 
-    // store the completed 16-byte chunks, then move the partial chunk to the staging base
+    // store the completed 16-byte chunks (staging chunks 1..nfl), then move the partial one
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
     const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + kEncGuard + 16u * c);
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (c < nfl) v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
         vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, v);
     }
-    if (nfl && lane == 0) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + kEncGuard + 16u * nfl);
-        *reinterpret_cast<u32x4*>(stage + kEncGuard) = v;
+    if (nfl && lane < 4u) {
+        u32* s32 = reinterpret_cast<u32*>(stage);
+        s32[4u + lane] = s32[4u * (nfl + 1u) + lane];
     }
     wave_lds_sync();
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
-    st.prev_top = t63;
+    st.prev_top = readlane(top, kOwnLanes - 1u);
     const u32 i63 = readlane(incl, 63);
     st.rs = i63 > st.rs ? i63 : st.rs;
     return rounds;
@@ -313,12 +315,12 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_off,
                                                         uint64_t* __restrict__ out_len,
                                                         uint32_t* __restrict__ status, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 3 * kTile];
-    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kWavesPerBlock * (kEncRing + kEncGuard)];
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kWavesPerBlock * kEncStage];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
-    uint8_t* stage = stage_all + wid * (kEncRing + kEncGuard);
-    const uint8_t* slots = slots_all + wid * 3 * kTile;
+    uint8_t* stage = stage_all + wid * kEncStage;
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
     const u32 nw = gridDim.x * kWavesPerBlock;
 
     for (u32 b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
@@ -338,11 +340,11 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
         const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U + U / 2u);
         EncState st{0u, 0u, 0u, 0u};
-        walk_tiles(rsi, (U + kTile - 1u) / kTile, lane, slots, [&](u32 t, const uint8_t* cs, const uint8_t* ns) {
-            return enc_tile(cs, ns, t * kTile, U, lane, stage, rso, st);
+        walk_tiles(rsi, ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs) {
+            return enc_tile(cs, t * kTileStep, U, lane, stage, rso, st);
         });
-        // the final partial chunk (< 16 bytes): byte stores, nothing past C is touched
-        if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[kEncGuard + lane];
+        // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
+        if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
         if (lane == 0) {
             out_len[b] = st.out_pos;
             if (status) status[b] = RLE_STATUS_OK;
@@ -369,94 +371,86 @@ __device__ __forceinline__ uint2 dec_table_entry(u32 e) {
     return make_uint2(masks, exits);
 }
 
+// Staging (per wave): decoded position r (biased by 16: chunk 0 is never stored) holds a u16:
+// 0 = no token starts here, else 0x8000 | (r & 15) << 8 | byte at a token start.  Within a
+// 16-aligned chunk the keys grow with position (and survive moving the chunk), so a packed-u16
+// prefix max fills each run from its start.  Chunks sit at a 36-byte stride (16 x 2 B + 4 B pad) against bank conflicts.
+constexpr u32 kDecChunks = 192;              // >= ceil((16 + 15 + 3024 + 1) / 16)
+constexpr u32 kDecStage = 36u * kDecChunks;  // bytes per wave
+__device__ __forceinline__ u32 dpad(u32 r) { return 2u * r + ((r >> 4) << 2); }
+
 struct DecState {
     u32 out_pos;   // decoded bytes produced so far
-    u32 flushed;   // decoded bytes already stored (multiple of 16); staging base
+    u32 flushed;   // decoded bytes already stored (multiple of 16); staging chunk 1 = flushed
     u32 d;         // offset of the first token start in the current tile (0..2)
-    u32 fillc;     // 0x100|byte of the last stored position (run continuation carry)
+    u32 fillc;     // byte of the last stored position (run continuation carry)
     u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
     u32 serial;    // 1 -> stream needs the exact serial path
 };
 
-// Store chunks [0, nch) (relative to st.flushed); chunks < nstaged are read from staging, the
-// rest hold no token start.  Staging holds 0x100|byte at token starts and 0 elsewhere; each
-// run is filled forward from its start; positions >= `valid` take `tailv`.  Read chunks are
-// re-zeroed.  Returns the number of store instructions issued.
-__device__ __forceinline__ u32 dec_flush(u32 nch, u32 nstaged, u32 valid, u32 tailv, u32 lane, uint16_t* stage,
-                                         u32x4 rso, u32 flushed, u32& fillc) {
-    const u32 rounds = (nch + kWave - 1u) / kWave;
+// Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
+__device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc) {
+    const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
-        const bool active = c < nch;
-        const bool staged = active && c < nstaged;
-        u32x4 v0 = u32x4{0u, 0u, 0u, 0u}, v1 = u32x4{0u, 0u, 0u, 0u};
-        if (staged) {
-            v0 = *reinterpret_cast<const u32x4*>(stage + 16u * c);
-            v1 = *reinterpret_cast<const u32x4*>(stage + 16u * c + 8u);
-        }
-        const u32 L[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        u32 f[16];
-        u32 cur = 0;
+        const bool active = c < nfl;
+        u32* s32 = reinterpret_cast<u32*>(stage + 36u * (c + 1u));
+        u32 L[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        if (active) {
 #pragma unroll
-        for (u32 j = 0; j < 16; ++j) {
-            const u32 h = (j & 1u) ? (L[j >> 1] >> 16) : (L[j >> 1] & 0xFFFFu);
-            cur = h ? h : cur;
-            f[j] = cur;
+            for (u32 m = 0; m < 8; ++m) L[m] = s32[m];
         }
-        const u32 lastp = active ? cur : 0u;
-        const u32 incl = wave_scan_incl(lastp, 0u, OpLatest());
+        // prefix max of the keys inside the chunk: within each pair, then across pairs
+#pragma unroll
+        for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
+#pragma unroll
+        for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m - 1], L[m - 1], 0x03020302u));
+        const u32 lastk = L[7] >> 16;
+        const u32 lv = (lastk & 0x8000u) ? (0x100u | (lastk & 0xFFu)) : 0u;
+        const u32 incl = wave_scan_incl(lv, 0u, OpLatest());
         const u32 before = from_prev_lane(incl, 0u);
-        const u32 carry = before ? before : fillc;
-        u32 ob[4] = {0u, 0u, 0u, 0u};
-        const u32 pbase = 16u * c;
-#pragma unroll
-        for (u32 j = 0; j < 16; ++j) {
-            const u32 val = (pbase + j) < valid ? ((f[j] ? f[j] : carry) & 0xFFu) : tailv;
-            ob[j >> 2] |= val << (8u * (j & 3u));
-        }
+        const u32 carry = (before ? before : fillc) & 0xFFu;
+        const u32 crep = carry * 0x00010001u;
         u32x4 o;
-        o.x = ob[0]; o.y = ob[1]; o.z = ob[2]; o.w = ob[3];
-        vstore(rso, active ? flushed + pbase : kOOB, o);
-        if (staged) {
-            *reinterpret_cast<u32x4*>(stage + 16u * c) = u32x4{0u, 0u, 0u, 0u};
-            *reinterpret_cast<u32x4*>(stage + 16u * c + 8u) = u32x4{0u, 0u, 0u, 0u};
+        o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
+        o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
+        o.z = __builtin_amdgcn_perm(pkmax(L[5], crep), pkmax(L[4], crep), 0x06040200u);
+        o.w = __builtin_amdgcn_perm(pkmax(L[7], crep), pkmax(L[6], crep), 0x06040200u);
+        vstore(rso, active ? flushed + 16u * c : kOOB, o);
+        if (active) {
+#pragma unroll
+            for (u32 m = 0; m < 8; ++m) s32[m] = 0u;
         }
-        const u32 lastlane = (nch - 1u - k * kWave) < (kWave - 1u) ? (nch - 1u - k * kWave) : (kWave - 1u);
-        const u32 lv = readlane(f[15] ? f[15] : carry, lastlane);
-        fillc = lv;
+        const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
+        fillc = readlane(o.w >> 24, lastlane);
         wave_lds_sync();
     }
     return rounds;
 }
 
-__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const uint8_t* nslot, u32 pos, u32 C, u32 U,
-                                        u32 lane, const uint2* tbl, uint16_t* stage, uint16_t* trash, u32x4 rso,
-                                        DecState& st) {
+__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u32 U, u32 lane, const uint2* tbl,
+                                        uint8_t* stage, u32 trash_addr, u32x4 rso, DecState& st) {
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     const u32 p0 = pos + 16u * lane;
     const u32 left = p0 < C ? C - p0 : 0u;
     const u32 nl = left < 16u ? left : 16u;
-    const u32 validm = lowmask(nl);
+    const u32 validm = lane < kOwnLanes ? lowmask(nl) : 0u;
     u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
-    if (pos + kTile > C) {   // last tile: bytes at index >= C read as the stream's zero padding
+    if (pos + kSlot > C) {   // last tiles: bytes at index >= C read as the stream's zero padding
 #pragma unroll
         for (u32 k = 0; k < 4; ++k) {
             const u32 nb = nl > 4u * k ? (nl - 4u * k < 4u ? nl - 4u * k : 4u) : 0u;
             w[k] &= lowmask(8u * nb);
         }
     }
-    // 2-byte lookahead: next lane's first bytes; lane 63 reads the next tile
-    const u32 pn = pos + kTile;
-    const u32 nvn = pn < C ? ((C - pn) < 2u ? (C - pn) : 2u) : 0u;
-    const u32 nx = uniform(*reinterpret_cast<const u32*>(nslot)) & lowmask(8u * nvn);
-    const u32 la = from_next_lane(w[0] & 0xFFFFu, nx) & 0xFFFFu;
+    const u32 la = from_next_lane(w[0] & 0xFFFFu, 0u) & 0xFFFFu;   // 2-byte lookahead
 
     // E bit j <=> y[j] == y[j+1]  (a token starting at j is then 3 bytes long)
     const u32 NE = nz4(w[0] ^ alignbyte(w[1], w[0], 1)) | (nz4(w[1] ^ alignbyte(w[2], w[1], 1)) << 4) |
                    (nz4(w[2] ^ alignbyte(w[3], w[2], 1)) << 8) | (nz4(w[3] ^ alignbyte(la, w[3], 1)) << 12);
     const u32 E = ~NE & 0xFFFFu;
     const uint2 ta = tbl[E & 0xFFu], tb = tbl[E >> 8];
-    const u32 map = __builtin_amdgcn_perm(tb.y, tb.y, ta.y);
+    const u32 map = lane < kOwnLanes ? __builtin_amdgcn_perm(tb.y, tb.y, ta.y) : kMapId;
     const u32 incl = wave_scan_incl(map, kMapId, OpMap());
     const u32 excl = from_prev_lane(incl, kMapId);
     const u32 dl = bfe(excl, 8u * st.d, 8);
@@ -472,15 +466,16 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const uint8_t* nsl
     const u32 PF = P & ~(v18 >> 2);
     const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
                        alignbyte(la, w[3], 2)};
-    u32 dm1[4], extra = 0, badb = 0;
+    u32 W[4], extra = 0, badb = 0;
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 mpb = nib_to_bytes(bfe(MP, 4u * k, 4));
         const u32 dor = dg[k] | 0x80808080u;
         const u32 lo = dor - 0x31313131u, hi = dor - 0x3A3A3A3Au;
-        dm1[k] = lo & 0x7F7F7F7Fu;   // d - '1' for d in ['1', 0x80)
-        extra = __builtin_amdgcn_udot4(dm1[k], mpb, extra, false);
+        const u32 dm1 = lo & 0x7F7F7F7Fu & (mpb * 0xFFu);   // d - '1' at pair starts
+        extra = __builtin_amdgcn_udot4(dm1, 0x01010101u, extra, false);
         badb |= (~lo | hi | dg[k]) & (mpb << 7);
+        W[k] = nib_to_bytes(bfe(S, 4u * k, 4)) + dm1;        // decoded length per position
     }
     const u32 nout = bcnt(S, extra);
     const bool serial_lane = badb != 0u || (PF & (v18 >> 1)) != 0u;
@@ -497,27 +492,35 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const uint8_t* nsl
         st.tail = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
     }
 
-    // scatter 0x100|byte at each token start's decoded position; non-starts write a private slot
+    // scatter a key at each token start's decoded position; other positions write a private
+    // slot.  o2 = 2 x position; odd positions store the key from the high half (d16_hi).
     const u32 rel0 = st.out_pos - st.flushed;
-    u32 o = rel0 + oincl - nout;
-    uint16_t* tr = trash + lane;
+    u32 o2 = 2u * (16u + rel0 + oincl - nout);
+    const u32 sbase = lds_addr(stage);
+    u32 xk[8];   // 0x8000 | byte, two positions per dword
+#pragma unroll
+    for (u32 m = 0; m < 8; ++m) xk[m] = __builtin_amdgcn_perm(0x80808080u, w[m >> 1], (m & 1u) ? 0x04030402u : 0x04010400u);
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) W[k] *= 2u;
 #pragma unroll
     for (u32 j = 0; j < 16; ++j) {
-        const u32 sbit = bfe(S, j, 1);
-        uint16_t* p = sbit ? stage + o : tr;
-        *p = (uint16_t)(0x100u | bfe(w[j >> 2], 8u * (j & 3u), 8));
-        o += sbit + bfe(MP, j, 1) * bfe(dm1[j >> 2], 8u * (j & 3u), 8);
+        const u32 w2 = (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+        const u32 a = w2 ? sbase + o2 + ((o2 >> 3) & ~3u) : trash_addr;
+        auto* p = reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(a);
+        if (j & 1u) *p = (uint16_t)((((o2 << 23) & 0x0F000000u) | xk[j >> 1]) >> 16);
+        else *p = (uint16_t)(((o2 << 7) & 0x0F00u) | xk[j >> 1]);
+        o2 += w2;
     }
     wave_lds_sync();
 
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
-    const u32 rounds = dec_flush(nfl, nfl, newrel, 0u, lane, stage, rso, st.flushed, st.fillc);
-    if (nfl) {   // move the partial chunk to the staging base
-        if (lane < 2u) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16u * nfl + 8u * lane);
-            *reinterpret_cast<u32x4*>(stage + 8u * lane) = v;
-            *reinterpret_cast<u32x4*>(stage + 16u * nfl + 8u * lane) = u32x4{0u, 0u, 0u, 0u};
+    const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc);
+    if (nfl) {   // move the partial chunk to staging chunk 1
+        if (lane < 8u) {
+            u32* s32 = reinterpret_cast<u32*>(stage);
+            s32[9u + lane] = s32[9u * (nfl + 1u) + lane];
+            s32[9u * (nfl + 1u) + lane] = 0u;
         }
         wave_lds_sync();
     }
@@ -527,12 +530,50 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const uint8_t* nsl
     return rounds;
 }
 
+// After the last tile: outputs [flushed, U) = the partial chunk still staged (decoded positions
+// < out_pos), then zeros or the final unbounded token's byte.  Runs once per buffer.
+__device__ __forceinline__ void dec_finish(const DecState& st, u32 U, u32 lane, uint8_t* stage, u32x4 rso,
+                                           uint8_t* dst) {
+    const u32 rel = st.out_pos - st.flushed;   // < 16
+    const u32 span = U - st.flushed;
+    const u32 nq = (span + 15u) >> 4;
+    const u32 tv = st.tail & 0xFFu;
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stage + 36u);
+    for (u32 q0 = 0; q0 < nq; q0 += kWave) {
+        const u32 q = q0 + lane;
+        if (q < nq) {
+            u32 ob[4] = {0u, 0u, 0u, 0u};
+            u32 cur = st.fillc;
+            for (u32 j = 0; j < 16u; ++j) {
+                u32 v = tv;
+                if (q == 0u && j < rel) {
+                    const u32 h = s16[j];
+                    cur = (h & 0x8000u) ? (h & 0xFFu) : cur;
+                    v = cur;
+                }
+                ob[j >> 2] |= v << (8u * (j & 3u));
+            }
+            if (16u * q + 16u <= span) {
+                u32x4 o;
+                o.x = ob[0]; o.y = ob[1]; o.z = ob[2]; o.w = ob[3];
+                vstore(rso, st.flushed + 16u * q, o);
+            } else {
+                for (u32 j = 0; 16u * q + j < span; ++j)
+                    dst[st.flushed + 16u * q + j] = (uint8_t)(ob[j >> 2] >> (8u * (j & 3u)));
+            }
+        }
+    }
+    wave_lds_sync();
+    if (lane < 9u) reinterpret_cast<u32*>(stage)[9u + lane] = 0u;   // staging chunk 1 back to zero
+    vm_drain();
+}
+
 // Exact serial decode (src/rleCompression.c:47-62 semantics, writes capped at cap) for the
 // streams the tiled path declines: counts outside '1'..'9', unbounded counts before the last
 // token, or streams that decode to more than U bytes.  One lane; the encoder never emits these.
 __device__ u32 dec_serial(const uint8_t* src, u32 C, u32 U, uint64_t cap, uint8_t* dst, u32 lane,
-                          uint16_t* stage) {
-    for (u32 k = lane; k < kDecRing * 2u / 16u; k += kWave)
+                          uint8_t* stage) {
+    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     for (uint64_t c = lane; c * 16u < cap; c += kWave) {
         if (c * 16u + 16u <= cap) *reinterpret_cast<u32x4*>(dst + c * 16u) = u32x4{0u, 0u, 0u, 0u};
@@ -575,17 +616,17 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_len,
                                                         const uint64_t* __restrict__ out_cap,
                                                         uint32_t* __restrict__ status, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 3 * kTile];
-    __shared__ __attribute__((aligned(16))) uint16_t stage_all[kWavesPerBlock * kDecRing];
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kWavesPerBlock * kDecStage];
     __shared__ __attribute__((aligned(16))) uint16_t trash_all[kWavesPerBlock * kWave];
     __shared__ uint2 tbl[256];
     tbl[threadIdx.x] = dec_table_entry(threadIdx.x);
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
-    uint16_t* stage = stage_all + wid * kDecRing;
-    uint16_t* trash = trash_all + wid * kWave;
-    const uint8_t* slots = slots_all + wid * 3 * kTile;
-    for (u32 k = lane; k < kDecRing * 2u / 16u; k += kWave)
+    uint8_t* stage = stage_all + wid * kDecStage;
+    const u32 trash_addr = lds_addr(trash_all + wid * kWave + lane);
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     const u32 nw = gridDim.x * kWavesPerBlock;
@@ -606,34 +647,12 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
         DecState st{0u, 0u, 0u, 0u, 0u, 0u};
-        walk_tiles(rsi, (C + kTile - 1u) / kTile, lane, slots, [&](u32 t, const uint8_t* cs, const uint8_t* ns) {
-            return dec_tile(cs, ns, t * kTile, C, U, lane, tbl, stage, trash, rso, st);
+        walk_tiles(rsi, ntiles_for(C), lane, slots, [&](u32 t, const uint8_t* cs) {
+            return dec_tile(cs, t * kTileStep, C, U, lane, tbl, stage, trash_addr, rso, st);
         });
         u32 stat = RLE_STATUS_OK;
-        if (st.serial) {
-            stat = dec_serial(src, C, U, cap, dst, lane, stage);
-        } else {
-            // the partial chunk still staged, then [out_pos, U): zeros, or the final
-            // unbounded token's byte; the chunk holding U is written byte by byte
-            const u32 rel = st.out_pos - st.flushed;   // staged positions (chunk 0 only)
-            const u32 span = U - st.flushed;
-            const u32 full = span >> 4, tailn = span & 15u;
-            const u32 tv = st.tail & 0xFFu;
-            dec_flush(full, 1u, rel, tv, lane, stage, rso, st.flushed, st.fillc);
-            if (tailn) {
-                u32 v = st.fillc;
-                if (full == 0u)
-                    for (u32 j = 0; j <= lane && j < 16u; ++j) {
-                        const u32 hj = stage[j];
-                        v = hj ? hj : v;
-                    }
-                const u32 p = 16u * full + lane;
-                if (lane < tailn) dst[st.flushed + p] = (uint8_t)(p < rel ? (v & 0xFFu) : tv);
-                wave_lds_sync();
-                if (full == 0u && lane < 2u) reinterpret_cast<u32x4*>(stage)[lane] = u32x4{0u, 0u, 0u, 0u};
-            }
-            vm_drain();
-        }
+        if (st.serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
+        else dec_finish(st, U, lane, stage, rso, dst);
         if (lane == 0 && status) status[b] = stat;
         wave_lds_sync();
     }
@@ -783,4 +802,4 @@ extern "C" int rle_mi355x_device_count(void) {
     return n;
 }
 
-extern "C" const char* rle_mi355x_version(void) { return "rle_mi355x 0.2 (gfx950, wave-per-buffer tiled codec)"; }
+extern "C" const char* rle_mi355x_version(void) { return "rle_mi355x 0.3 (gfx950, wave-per-buffer tiled codec)"; }
