@@ -28,6 +28,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import rle_mi355x as R  # noqa: E402
+import shard  # noqa: E402
 
 METRIC = "GiB/s RLE encode+decode, device-resident, batched 4–256 KiB buffers"
 GIB = float(1 << 30)
@@ -74,7 +75,7 @@ class Batch:
     def __init__(self, wl, rank, world, dev):
         n = wl["n"]
         kinds = wl["kinds"]
-        gidx = [k * world + rank for k in range(n)]
+        gidx = [k * world + rank for k in range(n)]   # shard.shard_indices(n * world, rank, world)
         sizes = [wl["size"] if wl["size"] else mixed_size(i) for i in gidx]
         offs, total = R.layout(sizes)
         coffs, ctotal = R.compressed_slots(sizes)
@@ -99,16 +100,6 @@ class Batch:
     def decode(self, stream=None):
         R.decode_batch(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
                        stream=stream)
-
-
-def gather_global_offsets(clen, world):
-    """RCCL all-gather of the per-buffer compressed sizes, then the exclusive scan in global
-    (round-robin) order: global buffer i = k * world + rank."""
-    n = clen.numel()
-    g = torch.empty(world * n, dtype=clen.dtype, device=clen.device)
-    dist.all_gather_into_tensor(g, clen)
-    glob = g.view(world, n).t().reshape(-1)           # global order
-    return torch.cumsum(glob, 0) - glob               # exclusive scan
 
 
 def time_kernels(fn, reps, stream):
@@ -173,8 +164,8 @@ def main():
 
     def step():
         B.encode(stream)
-        if world > 1:
-            gather_global_offsets(B.clen, world)
+        if world > 1:   # the one exchange step: sizes all-gathered over RCCL, scanned in global order
+            shard.global_offsets(B.clen, world)
         B.decode(stream)
 
     for _ in range(max(1, args.warmup)):

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 
 #include "rleCompression.h"
 #include "rle_mi355x.h"
@@ -30,6 +31,18 @@ int g_ndev = 0;
 int g_dev_pin = -1;
 std::atomic<unsigned> g_next_dev{0};
 std::atomic<int> g_warned_overflow{0};
+
+// Host-path accounting (rle_mi355x_dropin_stats): bytes moved and wall time per phase.
+struct Stats {
+    std::atomic<uint64_t> calls_compress{0}, calls_decompress{0};
+    std::atomic<uint64_t> bytes_in{0}, bytes_out{0};        // caller bytes in / returned bytes out
+    std::atomic<uint64_t> bytes_h2d{0}, bytes_d2h{0};
+    std::atomic<uint64_t> ns_stage_in{0}, ns_device{0}, ns_stage_out{0};
+} g_stats;
+inline uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 [[noreturn]] void die(const char* what, hipError_t e) {
     fprintf(stderr, "librle_mi355x: %s failed: %s\n", what, hipGetErrorString(e));
@@ -129,7 +142,9 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
     grow_host(c->h_in, c->h_in_cap, U);
     grow_dev(c->d_in, c->d_in_cap, round16(U));
     grow_dev(c->d_out, c->d_out_cap, round16(maxC));
+    const uint64_t t0 = now_ns();
     memcpy(c->h_in, data, U);
+    const uint64_t t1 = now_ns();
     c->h_meta[0] = 0; c->h_meta[1] = U; c->h_meta[2] = 0; c->h_meta[3] = 0;
     check(hipMemcpyAsync(c->d_in, c->h_in, U, hipMemcpyHostToDevice, c->s), "H2D");
     check(hipMemcpyAsync(c->d_meta, c->h_meta, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
@@ -150,6 +165,7 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
         check(hipMemcpyAsync(c->h_out, c->d_out, C, hipMemcpyDeviceToHost, c->s), "D2H");
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     }
+    const uint64_t t2 = now_ns();
     char* r = static_cast<char*>(malloc(C + 16));
     if (!r) {
         *compressedSize = C;
@@ -158,6 +174,15 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
     memcpy(r, c->h_out, C);
     memset(r + C, 0, 16);
     *compressedSize = C;
+    const uint64_t t3 = now_ns();
+    g_stats.calls_compress++;
+    g_stats.bytes_in += U;
+    g_stats.bytes_out += C;
+    g_stats.bytes_h2d += U;
+    g_stats.bytes_d2h += one_trip ? maxC : C;
+    g_stats.ns_stage_in += t1 - t0;
+    g_stats.ns_device += t2 - t1;
+    g_stats.ns_stage_out += t3 - t2;
     return r;
 }
 
@@ -175,7 +200,9 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     grow_host(c->h_out, c->h_out_cap, total);
     grow_dev(c->d_in, c->d_in_cap, round16(C));
     grow_dev(c->d_out, c->d_out_cap, round16(total));
+    const uint64_t t0 = now_ns();
     memcpy(c->h_in, data, C);
+    const uint64_t t1 = now_ns();
     c->h_meta[0] = 0; c->h_meta[1] = C; c->h_meta[2] = 0; c->h_meta[3] = U; c->h_meta[4] = total; c->h_meta[5] = 0;
     check(hipMemcpyAsync(c->d_in, c->h_in, C, hipMemcpyHostToDevice, c->s), "H2D");
     check(hipMemcpyAsync(c->d_meta, c->h_meta, 6 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
@@ -187,6 +214,7 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     if (U) check(hipMemcpyAsync(c->h_out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     const uint32_t st = (uint32_t)c->h_meta[5];
+    const uint64_t t2 = now_ns();
     memcpy(r, c->h_out, U);
     if (E) {
         if (st & RLE_STATUS_SERIAL) {  // a non-encoder stream may have written into the E region
@@ -200,5 +228,57 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     if ((st & RLE_STATUS_OVERFLOW) && !g_warned_overflow.exchange(1))
         fprintf(stderr, "librle_mi355x: RLEdecompress: stream decodes past U+E (the reference would overflow its "
                         "heap block); output truncated\n");
+    const uint64_t t3 = now_ns();
+    g_stats.calls_decompress++;
+    g_stats.bytes_in += C;
+    g_stats.bytes_out += total;
+    g_stats.bytes_h2d += C;
+    g_stats.bytes_d2h += U;
+    g_stats.ns_stage_in += t1 - t0;
+    g_stats.ns_device += t2 - t1;
+    g_stats.ns_stage_out += t3 - t2;
     return r;
 }
+
+extern "C" int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset) {
+    if (!out) return RLE_E_INVAL;
+    out->calls_compress = g_stats.calls_compress.load();
+    out->calls_decompress = g_stats.calls_decompress.load();
+    out->bytes_in = g_stats.bytes_in.load();
+    out->bytes_out = g_stats.bytes_out.load();
+    out->bytes_h2d = g_stats.bytes_h2d.load();
+    out->bytes_d2h = g_stats.bytes_d2h.load();
+    out->ns_stage_in = g_stats.ns_stage_in.load();
+    out->ns_device = g_stats.ns_device.load();
+    out->ns_stage_out = g_stats.ns_stage_out.load();
+    if (reset) {
+        g_stats.calls_compress = 0; g_stats.calls_decompress = 0; g_stats.bytes_in = 0; g_stats.bytes_out = 0;
+        g_stats.bytes_h2d = 0; g_stats.bytes_d2h = 0; g_stats.ns_stage_in = 0; g_stats.ns_device = 0;
+        g_stats.ns_stage_out = 0;
+    }
+    return RLE_OK;
+}
+
+namespace {
+// RLE_MI355X_STATS=<path>: the drop-in's host-path accounting is written there as JSON at exit
+// (used to record the server's host<->device rate).
+struct StatsAtExit {
+    ~StatsAtExit() {
+        const char* path = getenv("RLE_MI355X_STATS");
+        if (!path || !*path) return;
+        rle_dropin_stats_t s;
+        rle_mi355x_dropin_stats(&s, 0);
+        FILE* f = fopen(path, "w");
+        if (!f) return;
+        fprintf(f,
+                "{\"calls_compress\": %llu, \"calls_decompress\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, "
+                "\"bytes_h2d\": %llu, \"bytes_d2h\": %llu, \"ns_stage_in\": %llu, \"ns_device\": %llu, "
+                "\"ns_stage_out\": %llu}\n",
+                (unsigned long long)s.calls_compress, (unsigned long long)s.calls_decompress,
+                (unsigned long long)s.bytes_in, (unsigned long long)s.bytes_out, (unsigned long long)s.bytes_h2d,
+                (unsigned long long)s.bytes_d2h, (unsigned long long)s.ns_stage_in, (unsigned long long)s.ns_device,
+                (unsigned long long)s.ns_stage_out);
+        fclose(f);
+    }
+} g_stats_at_exit;
+}  // namespace

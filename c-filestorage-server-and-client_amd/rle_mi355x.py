@@ -32,6 +32,15 @@ class RLEError(RuntimeError):
     pass
 
 
+class DropinStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("calls_compress", "calls_decompress", "bytes_in", "bytes_out",
+                                               "bytes_h2d", "bytes_d2h", "ns_stage_in", "ns_device",
+                                               "ns_stage_out")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
 def lib():
     """Load (once) and return the codec library."""
     global _lib
@@ -55,6 +64,8 @@ def lib():
     L.rle_mi355x_device_count.argtypes = []
     L.rle_mi355x_version.restype = ctypes.c_char_p
     L.rle_mi355x_version.argtypes = []
+    L.rle_mi355x_dropin_stats.restype = ctypes.c_int
+    L.rle_mi355x_dropin_stats.argtypes = [ctypes.POINTER(DropinStats), ctypes.c_int]
     L.RLEcompress.restype = ctypes.c_void_p
     L.RLEcompress.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.RLEdecompress.restype = ctypes.c_void_p
@@ -155,3 +166,12 @@ def device_count() -> int:
 
 def version() -> str:
     return lib().rle_mi355x_version().decode()
+
+
+def dropin_stats(reset=False) -> dict:
+    """Host-path accounting of the drop-in calls made in this process (include/rle_mi355x.h)."""
+    st = DropinStats()
+    rc = lib().rle_mi355x_dropin_stats(ctypes.byref(st), 1 if reset else 0)
+    if rc != RLE_OK:
+        raise RLEError(f"rle_mi355x_dropin_stats failed: {rc}")
+    return st.as_dict()

@@ -1,0 +1,39 @@
+"""Sharding of a batch of independent buffers across the GPUs of one node.
+
+Every buffer of the reference codec is independent (src/rleCompression.c keeps no state across
+calls), so a global batch shards with no data-path collective: buffer i goes to rank i % N
+(round-robin) and is encoded, stored and decoded on that GPU.  The one exchange step is the
+all-gather of the per-buffer compressed sizes (u64), after which every rank can place any
+buffer's compressed stream in the global, buffer-ordered stream (an exclusive scan in global
+order).  With the NCCL backend torch.distributed runs this over RCCL / xGMI; the payloads stay
+where they are.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_indices(n_global: int, rank: int, world: int):
+    """Global buffer indices owned by `rank` (round-robin: i % world == rank), in local order."""
+    return list(range(rank, n_global, world))
+
+
+def local_count(n_global: int, rank: int, world: int) -> int:
+    return (n_global - rank + world - 1) // world if rank < n_global else 0
+
+
+def global_offsets(local_sizes: torch.Tensor, world: int) -> torch.Tensor:
+    """All-gather per-buffer compressed sizes (int64, one per local buffer, every rank holding the
+    same count) and return the exclusive scan of all sizes in global order: entry i is the byte
+    offset of global buffer i in the concatenated stream.  Collective: every rank must call it."""
+    n = local_sizes.numel()
+    if world == 1:
+        return torch.cumsum(local_sizes, 0) - local_sizes
+    gathered = torch.empty(world * n, dtype=local_sizes.dtype, device=local_sizes.device)
+    dist.all_gather_into_tensor(gathered, local_sizes.contiguous())
+    glob = gathered.view(world, n).t().reshape(-1)   # global order: i = k * world + r
+    return torch.cumsum(glob, 0) - glob
+
+
+def my_offsets(glob_offsets: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """This rank's buffers' offsets in the global stream."""
+    return glob_offsets[rank::world]

@@ -67,6 +67,17 @@ int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const ui
 int rle_gen_synthetic_device(void* d_out, const uint64_t* d_off, const uint64_t* d_len,
                              const uint32_t* d_kind, const uint64_t* d_index, uint32_t n, void* stream);
 
+/* Host-path accounting of the drop-in RLEcompress/RLEdecompress (process-wide): bytes the callers
+ * passed in and got back, bytes moved host->device / device->host, and wall time spent staging
+ * into pinned memory, on the device round trip (H2D + kernel + D2H, stream-synchronised) and
+ * copying out to the caller's malloc block.  reset != 0 zeroes the counters after reading. */
+typedef struct {
+    uint64_t calls_compress, calls_decompress;
+    uint64_t bytes_in, bytes_out, bytes_h2d, bytes_d2h;
+    uint64_t ns_stage_in, ns_device, ns_stage_out;
+} rle_dropin_stats_t;
+int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
+
 /* Runs the cross-lane (DPP) primitive self-test on the current device; 0 = pass. */
 int rle_mi355x_selftest(void);
 

@@ -148,7 +148,7 @@ def main():
     # reference fixture files
     D = {"files": []}
     os.makedirs(os.path.join(HERE, "dummyFiles"), exist_ok=True)
-    keep = {"file1", "file2", "rec/rec1", "rec/rec2", "smallfiles/small1", "smallfiles/small7"}
+    keep = {"file1", "file2", "rec/rec1", "rec/rec2", "smallfiles/small1", "smallfiles/small7", "bigfiles/randbig"}
     for root, _, files in os.walk(REF_FILES):
         for fn in sorted(files):
             p = os.path.join(root, fn)

@@ -1,0 +1,158 @@
+"""End-to-end: the UNCHANGED reference server and client over their AF_UNIX socket, with the
+reference codec (server_ref, BASELINE configs[0]) and with librle_mi355x.so linked in its place
+(server_gpu, configs[4]); binaries from e2e/Makefile (built from /root/reference).
+
+Battery 1 follows tests/test1.sh:13,17 (write file1,file2 and read them back; write the rec
+directory and read everything back with -R 0) and checks what the reference's script never
+does: every returned file is byte-identical to its source, and the server's exit statistic
+"Max total storage size reached" is 363500 bytes (the sum of the compressed sizes).
+Battery 2 follows tests/test2.sh:6-30 (LRU eviction with MAXSTORAGECAP=1000000): big2 + randbig
+fit (942363 compressed bytes), writing big4 evicts randbig, which is decoded and shipped back
+(src/server.c:312-323) and must match its source.
+"""
+import json
+import os
+import re
+import shutil
+import signal
+import subprocess
+import time
+
+import pytest
+
+from conftest import GOLDEN, REPO
+
+BIN = os.path.join(REPO, "e2e", "_bin")
+CLIENT = os.path.join(BIN, "client")
+ANSI = re.compile(r"\x1b\[[0-9;]*m")
+
+
+def _need(exe):
+    if not (os.path.exists(exe) and os.path.exists(CLIENT)):
+        pytest.skip(f"{exe} not built (make -C e2e needs /root/reference)")
+
+
+def _stage_files(tmp):
+    d = os.path.join(tmp, "files")
+    for rel in ("file1", "file2", "rec/rec1", "rec/rec2", "bigfiles/randbig"):
+        dst = os.path.join(d, rel)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copyfile(os.path.join(GOLDEN, "dummyFiles", rel.replace("/", "__")), dst)
+    for rel in ("bigfiles/big2", "bigfiles/big4"):
+        with open(os.path.join(d, rel), "wb") as f:
+            f.write(bytes(360000))
+    return d
+
+
+class Server:
+    def __init__(self, exe, tmp, cfg, env=None):
+        self.tmp = tmp
+        self.sock = os.path.join(tmp, "s.sk")
+        conf = dict(cfg, SOCKETFILENAME=self.sock, LOGFILENAME=os.path.join(tmp, "logs.json"))
+        path = os.path.join(tmp, "config.txt")
+        with open(path, "w") as f:
+            f.write("".join(f"{k}={v}\n" for k, v in conf.items()))
+        self.p = subprocess.Popen([exe, path], cwd=tmp, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                  env=dict(os.environ, **(env or {})))
+        t0 = time.time()
+        while not os.path.exists(self.sock):
+            if self.p.poll() is not None or time.time() - t0 > 60:
+                raise RuntimeError("server did not start: " + self.p.stdout.read().decode(errors="replace"))
+            time.sleep(0.05)
+
+    def client(self, *args):
+        r = subprocess.run([CLIENT, "-f", self.sock, "-t", "0", *args], cwd=self.tmp, capture_output=True,
+                           timeout=120)
+        assert r.returncode == 0, (args, r.stdout.decode(errors="replace"), r.stderr.decode(errors="replace"))
+        return r
+
+    def stop(self):
+        self.p.send_signal(signal.SIGHUP)
+        out, _ = self.p.communicate(timeout=120)
+        return ANSI.sub("", out.decode(errors="replace"))
+
+
+def _max_storage(text):
+    m = re.search(r"Max total storage size reached: (\d+) bytes", text)
+    assert m, text[-2000:]
+    return int(m.group(1))
+
+
+def _returned(root):
+    out = {}
+    for d, _, fs in os.walk(root):
+        for fn in fs:
+            out.setdefault(fn, []).append(open(os.path.join(d, fn), "rb").read())
+    return out
+
+
+def battery1(exe, tmp, env=None):
+    files = _stage_files(tmp)
+    srv = Server(exe, tmp, {"MAXSTORAGECAP": 128000000, "MAXFILECOUNT": 10000, "WORKERPOOLSIZE": 1}, env)
+    t0 = time.perf_counter()
+    try:
+        f1, f2 = os.path.join(files, "file1"), os.path.join(files, "file2")
+        srv.client("-W", f"{f1},{f2}", "-r", f"{f1},{f2}", "-d", os.path.join(tmp, "dest1"))
+        srv.client("-w", f"{os.path.join(files, 'rec')},0", "-R", "0", "-d", os.path.join(tmp, "dest2"))
+    finally:
+        wall = time.perf_counter() - t0
+        text = srv.stop()
+    return _max_storage(text), _returned(os.path.join(tmp, "dest1")), _returned(os.path.join(tmp, "dest2")), wall
+
+
+def battery2(exe, tmp, env=None):
+    files = _stage_files(tmp)
+    srv = Server(exe, tmp, {"MAXSTORAGECAP": 1000000, "MAXFILECOUNT": 10, "WORKERPOOLSIZE": 4,
+                            "REPLACEMENTALGO": 1}, env)
+    b = lambda n: os.path.join(files, "bigfiles", n)
+    try:
+        srv.client("-W", f"{b('big2')},{b('randbig')}")
+        time.sleep(1.1)   # the LRU clock has 1-second resolution (tests/test2.sh:18)
+        srv.client("-r", b("big2"), "-d", os.path.join(tmp, "readback"))
+        srv.client("-W", b("big4"), "-D", os.path.join(tmp, "evicted1"))
+    finally:
+        text = srv.stop()
+    return _max_storage(text), _returned(os.path.join(tmp, "evicted1")), _returned(os.path.join(tmp, "readback"))
+
+
+def _src(name):
+    if name in ("big2", "big4"):
+        return bytes(360000)
+    rel = {"file1": "file1", "file2": "file2", "rec1": "rec/rec1", "rec2": "rec/rec2", "randbig": "bigfiles/randbig"}
+    return open(os.path.join(GOLDEN, "dummyFiles", rel[name].replace("/", "__")), "rb").read()
+
+
+def _check_battery1(res):
+    stat, d1, d2, _ = res
+    assert stat == 363500
+    assert sorted(d1) == ["file1", "file2"] and sorted(d2) == ["file1", "file2", "rec1", "rec2"]
+    for d in (d1, d2):
+        for name, blobs in d.items():
+            assert all(b == _src(name) for b in blobs), name
+
+
+def _check_battery2(res):
+    stat, ev, rb = res
+    assert stat == 942363
+    assert list(ev) == ["randbig"] and ev["randbig"] == [_src("randbig")]
+    assert rb["big2"] == [bytes(360000)]
+
+
+def test_e2e_reference_server(tmp_path):
+    exe = os.path.join(BIN, "server_ref")
+    _need(exe)
+    _check_battery1(battery1(exe, str(tmp_path / "b1")))
+    _check_battery2(battery2(exe, str(tmp_path / "b2")))
+
+
+@pytest.mark.gpu
+def test_e2e_gpu_server(tmp_path):
+    exe = os.path.join(BIN, "server_gpu")
+    _need(exe)
+    stats = str(tmp_path / "dropin_stats.json")
+    res1 = battery1(exe, str(tmp_path / "b1"), {"RLE_MI355X_STATS": stats})
+    _check_battery1(res1)
+    st = json.load(open(stats))
+    assert st["calls_compress"] >= 6 and st["calls_decompress"] >= 6
+    _check_battery2(battery2(exe, str(tmp_path / "b2")))
+    print("e2e gpu battery1 wall %.3fs dropin %s" % (res1[3], st))
