@@ -153,6 +153,6 @@ def test_e2e_gpu_server(tmp_path):
     res1 = battery1(exe, str(tmp_path / "b1"), {"RLE_MI355X_STATS": stats})
     _check_battery1(res1)
     st = json.load(open(stats))
-    assert st["calls_compress"] >= 6 and st["calls_decompress"] >= 6
+    assert st["calls_compress"] >= 4 and st["calls_decompress"] >= 6   # 4 writes; 6 reads
     _check_battery2(battery2(exe, str(tmp_path / "b2")))
     print("e2e gpu battery1 wall %.3fs dropin %s" % (res1[3], st))
