@@ -62,6 +62,11 @@ WORKLOADS = {
                       "encode+decode round trip"),
     "dec64k": dict(n=16384, size=65536, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
                    desc="16384 x 64 KiB per GPU (zero / random / runs50 / runs90), encode+decode round trip"),
+    # per-kind 64 KiB batches (profiling: tile cost per data kind)
+    "k64_zero": dict(n=16384, size=65536, kinds=(0,), ref_kinds="0", desc="16384 x 64 KiB zero"),
+    "k64_random": dict(n=16384, size=65536, kinds=(1,), ref_kinds="1", desc="16384 x 64 KiB random"),
+    "k64_runs50": dict(n=16384, size=65536, kinds=(2,), ref_kinds="2", desc="16384 x 64 KiB runs50"),
+    "k64_runs90": dict(n=16384, size=65536, kinds=(3,), ref_kinds="3", desc="16384 x 64 KiB runs90"),
     "mixed": dict(n=1024, size=None, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
                   desc="configs[2]: 1024 mixed 4 KiB-1 MiB buffers per GPU (zero / random / runs50 / runs90)"),
     "cfg3": dict(n=131072, size=65536, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",

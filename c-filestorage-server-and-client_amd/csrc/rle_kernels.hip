@@ -8,9 +8,9 @@
 //           (signed char)y[j+2]-'0'-1 copies, capped at U      — src/rleCompression.c:50-60
 //
 // Execution model: one wave64 owns one buffer and walks it in 1 KiB tiles,
-// 16 bytes per lane.  Loads are range-checked buffer_load_dwordx4 kept three tiles deep in
-// registers; their completion is counted by hand (s_waitcnt vmcnt(N), N = the stores issued
-// since), because hipcc's own bookkeeping drains the queue at every loop header once a
+// 16 bytes per lane.  Loads are range-checked LDS-DMA buffer_load_dwordx4 (two slots, two tiles
+// in flight); their completion is counted by hand (s_waitcnt vmcnt(N), N = the memory ops
+// issued since), because hipcc's own bookkeeping drains the queue at every loop header once a
 // variable number of stores sits in the loop.  Run boundaries and token starts are 16-bit
 // per-lane masks from SWAR byte compares; the sequential state (encode: run start position;
 // decode: token phase 0..2 as a v_perm byte map) and output offsets cross lanes by DPP wave
@@ -28,9 +28,6 @@ typedef uint32_t u32;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr u32 kWave = 64;
-constexpr u32 kWavesPerBlock = 4;
-constexpr u32 kBlock = kWave * kWavesPerBlock;
-constexpr u32 kMaxBlocks = 8192;
 constexpr u32 kMaxBufferBytes = 0x7FFFFFF0u;   // per-buffer limit (32-bit in-buffer offsets)
 constexpr u32 kOOB = 0x80000000u;               // store offset dropped by the range check
 
@@ -99,6 +96,8 @@ __device__ __forceinline__ u32 nz4(u32 d) {
     t |= t >> 7;         // ... at bits 0, 1 and 16, 17
     return (t | (t >> 14)) & 0xFu;
 }
+// byte 0 of x in all four bytes (v_perm: selector bytes 0..3 pick bytes of the second operand)
+__device__ __forceinline__ u32 rep4(u32 x) { return __builtin_amdgcn_perm(0u, x, 0u); }
 __device__ __forceinline__ u32 lowmask(u32 nbits) { return nbits >= 32u ? ~0u : ((1u << nbits) - 1u); }
 __device__ __forceinline__ u32 alignbyte(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
 __device__ __forceinline__ u32 bfe(u32 v, u32 off, u32 w) { return __builtin_amdgcn_ubfe(v, off, w); }
@@ -142,7 +141,11 @@ __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
         : "v"(voff), "s"(lds), "s"(rs)
         : "memory");
 }
+#ifndef RLE_NOSTORE
+#define RLE_NOSTORE 0
+#endif
 __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v) {
+    if (RLE_NOSTORE) voff = 0x80000000u;   // diagnostic builds: every store dropped by the range check
     asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
 // wait until at most n vector-memory ops are outstanding
@@ -151,8 +154,9 @@ __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v) {
         asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
         break;
 __device__ __forceinline__ void vm_wait(u32 n) {
-    switch (n < 8u ? n : 8u) {
+    switch (n < 15u ? n : 15u) {
         RLE_VMW(0) RLE_VMW(1) RLE_VMW(2) RLE_VMW(3) RLE_VMW(4) RLE_VMW(5) RLE_VMW(6) RLE_VMW(7) RLE_VMW(8)
+        RLE_VMW(9) RLE_VMW(10) RLE_VMW(11) RLE_VMW(12) RLE_VMW(13) RLE_VMW(14) RLE_VMW(15)
         default: break;
     }
 }
@@ -161,31 +165,38 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 
 // Tiles overlap: tile t is input [1008 t, 1008 t + 1024); lanes 0..62 own its first 1008 bytes
 // and lane 63 holds the next tile's first 16 bytes (the lookahead of lane 62).  Each tile is one
-// LDS-DMA into one of two slots, issued one tile ahead.  step(t, slot) processes tile t and
-// returns the store instructions it issued (or ~0u to stop); the wait before a step counts
-// them, because they are younger than the load it needs.
+// LDS-DMA into one of two slots.  A step reads its slot once (one ds_read_b128 per lane) and then
+// calls next() to refill that slot with tile t+2, so two tiles are in flight behind the one being
+// processed.  step(t, slot, next) returns the store instructions it issued after next() (or ~0u to
+// stop).  Vector-memory ops complete in issue order, so the wait for tile t+1 (issued inside step
+// t-1, before that step's stores) leaves step t-1's stores, the refill and step t's stores in
+// flight.  Loads past the buffer (t+2 >= ntiles) are range-checked to zero and cost no traffic.
 constexpr u32 kOwnLanes = 63;
 constexpr u32 kTileStep = 16 * kOwnLanes;   // 1008
 constexpr u32 kSlot = 16 * kWave;           // 1024
+struct Refill {
+    u32x4 rs;
+    u32 voff;   // lane byte offset of tile t+2
+    u32 lds;    // slot LDS address
+    __device__ __forceinline__ void operator()() const { dma_tile(rs, voff, lds); }
+};
 template <class Step>
 __device__ __forceinline__ void walk_tiles(u32x4 rs, u32 ntiles, u32 lane, const uint8_t* slots, Step step) {
     const u32 lo = 16u * lane;
-    const uint8_t* s0 = slots;
-    const uint8_t* s1 = slots + kSlot;
-    const u32 l0 = uniform(lds_addr(s0)), l1 = l0 + kSlot;
+    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
     dma_tile(rs, lo, l0);
     dma_tile(rs, kTileStep + lo, l1);
-    u32 prev = 0;
+    u32 p1 = 0, p2 = 0;   // stores of the last step and of the one before
     for (u32 t = 0; t < ntiles; t += 2) {
-        vm_wait(prev + 1);
-        prev = step(t, s0);
-        if (prev == ~0u || t + 1 >= ntiles) break;
-        dma_tile(rs, (t + 2) * kTileStep + lo, l0);
-        vm_wait(prev + 1);
-        prev = step(t + 1, s1);
-        if (prev == ~0u) break;
-        dma_tile(rs, (t + 3) * kTileStep + lo, l1);
+        vm_wait(p2 + 1u + p1);
+        p2 = p1;
+        p1 = step(t, slots, Refill{rs, (t + 2u) * kTileStep + lo, l0});
+        if (p1 == ~0u || t + 1u >= ntiles) break;
+        vm_wait(p2 + 1u + p1);
+        p2 = p1;
+        p1 = step(t + 1u, slots + kSlot, Refill{rs, (t + 3u) * kTileStep + lo, l1});
+        if (p1 == ~0u) break;
     }
     vm_drain();
 }
@@ -196,6 +207,40 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32 pkmax(u32 a, u32 b) {
     return __builtin_bit_cast(u32, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
 }
+
+// ---------------------------------------------------------------- diagnostic stamps
+// RLE_STAMPS=1 builds (never the product library) sum s_memtime cycles per decode segment in
+// each wave and add them into g_stamps; rle_mi355x_stamps() reads the sums.  Read shares only:
+// each stamp drains the LDS queue (MI355X guide, "In-kernel stamps").
+#ifndef RLE_STAMPS
+#define RLE_STAMPS 0
+#endif
+#if RLE_STAMPS
+constexpr u32 kStampSegs = 8;
+__device__ unsigned long long g_stamps[kStampSegs + 1];
+struct Stamps {
+    uint64_t acc[kStampSegs];
+    uint64_t last;
+};
+__device__ __forceinline__ uint64_t memtime() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define RLE_STAMP(SP, I)                  \
+    do {                                  \
+        const uint64_t _t = memtime();    \
+        (SP).acc[I] += _t - (SP).last;    \
+        (SP).last = _t;                   \
+    } while (0)
+#else
+struct Stamps {};
+#define RLE_STAMP(SP, I) \
+    do {                 \
+    } while (0)
+#endif
 
 // ================================================================ ENCODE
 // Staging (per wave): output position r of the tile (biased by 16: chunk 0 is a guard for the
@@ -209,10 +254,11 @@ struct EncState {
     u32 rs;         // start position of the run holding input byte tile_pos-1
 };
 
-__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, u32 pos, u32 U, u32 lane, uint8_t* stage, u32x4 rso,
-                                        EncState& st) {
+__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 U, u32 lane,
+                                        uint8_t* stage, u32x4 rso, EncState& st) {
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+    next();   // the slot is free once read
     const u32 p0 = pos + 16u * lane;
     const u32 left = p0 < U ? U - p0 : 0u;
     const u32 nl = left < 16u ? left : 16u;
@@ -308,48 +354,67 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, u32 pos, u32 U, u3
     return rounds;
 }
 
-__global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint64_t* __restrict__ in_len,
-                                                        uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        uint64_t* __restrict__ out_len,
-                                                        uint32_t* __restrict__ status, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 2 * kSlot];
-    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kWavesPerBlock * kEncStage];
+#ifndef RLE_XCD_MAP
+#define RLE_XCD_MAP 1
+#endif
+constexpr u32 kXcds = 8;
+// Buffer of wave `wid` of workgroup `wg` when every XCD (workgroups are dealt to the 8 XCDs
+// round-robin) takes a contiguous slice of the batch instead of every 8th buffer: a batch whose
+// cost varies with a stride (e.g. i % 4) then still spreads evenly over the XCDs.
+__device__ __forceinline__ u32 xcd_buffer(u32 wg, u32 ngrid, u32 waves, u32 wid) {
+#if RLE_XCD_MAP
+    const u32 per = ngrid / kXcds;   // launcher makes ngrid a multiple of 8
+    return ((wg % kXcds) * per + wg / kXcds) * waves + wid;
+#else
+    (void)ngrid;
+    return wg * waves + wid;
+#endif
+}
+
+#ifndef RLE_ENC_WAVES
+#define RLE_ENC_WAVES 4
+#endif
+constexpr u32 kEncWaves = RLE_ENC_WAVES;
+constexpr u32 kEncBlock = kWave * kEncWaves;
+__global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __restrict__ in,
+                                                           const uint64_t* __restrict__ in_off,
+                                                           const uint64_t* __restrict__ in_len,
+                                                           uint8_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ out_off,
+                                                           uint64_t* __restrict__ out_len,
+                                                           uint32_t* __restrict__ status, uint32_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kEncWaves * kEncStage];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     uint8_t* stage = stage_all + wid * kEncStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    const u32 nw = gridDim.x * kWavesPerBlock;
-
-    for (u32 b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
-        const uint64_t U64 = in_len[b];
-        const uint8_t* src = in + in_off[b];
-        uint8_t* dst = out + out_off[b];
-        u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
-        if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
-        if (bad) {
-            if (lane == 0) {
-                out_len[b] = 0;
-                if (status) status[b] = bad;
-            }
-            continue;
-        }
-        const u32 U = (u32)U64;
-        const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
-        const u32x4 rso = make_rsrc(dst, U + U / 2u);
-        EncState st{0u, 0u, 0u, 0u};
-        walk_tiles(rsi, ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs) {
-            return enc_tile(cs, t * kTileStep, U, lane, stage, rso, st);
-        });
-        // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
-        if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
+    const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kEncWaves, wid);
+    if (b >= n) return;
+    const uint64_t U64 = in_len[b];
+    const uint8_t* src = in + in_off[b];
+    uint8_t* dst = out + out_off[b];
+    u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+    if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+    if (bad) {
         if (lane == 0) {
-            out_len[b] = st.out_pos;
-            if (status) status[b] = RLE_STATUS_OK;
+            out_len[b] = 0;
+            if (status) status[b] = bad;
         }
-        wave_lds_sync();
+        return;
+    }
+    const u32 U = (u32)U64;
+    const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U + U / 2u);
+    EncState st{0u, 0u, 0u, 0u};
+    walk_tiles(rsi, ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        return enc_tile(cs, nx, t * kTileStep, U, lane, stage, rso, st);
+    });
+    // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
+    if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
+    if (lane == 0) {
+        out_len[b] = st.out_pos;
+        if (status) status[b] = RLE_STATUS_OK;
     }
 }
 
@@ -357,19 +422,50 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
 // Token-phase table: for an 8-bit mask e of "byte j equals byte j+1" and entry offset d (the
 // first token start in the group, 0..2): .x byte d = token-start mask, .y byte d = offset of the
 // first start past the group (.y byte 3 = 3, so .y is a v_perm selector).
-__device__ __forceinline__ uint2 dec_table_entry(u32 e) {
-    u32 masks = 0, exits = 3u << 24;
-    for (u32 d = 0; d < 3; ++d) {
-        u32 s = d, m = 0;
-        while (s < 8) {
-            m |= 1u << s;
-            s += ((e >> s) & 1u) ? 3u : 1u;
+struct DecTable {
+    uint2 e[256];
+};
+constexpr DecTable make_dec_table() {
+    DecTable t{};
+    for (u32 e = 0; e < 256; ++e) {
+        u32 masks = 0, exits = 3u << 24;
+        for (u32 d = 0; d < 3; ++d) {
+            u32 s = d, m = 0;
+            while (s < 8) {
+                m |= 1u << s;
+                s += ((e >> s) & 1u) ? 3u : 1u;
+            }
+            masks |= m << (8u * d);
+            exits |= (s - 8u) << (8u * d);
         }
-        masks |= m << (8u * d);
-        exits |= (s - 8u) << (8u * d);
+        t.e[e].x = masks;
+        t.e[e].y = exits;
     }
-    return make_uint2(masks, exits);
+    return t;
 }
+__constant__ DecTable kDecTable = make_dec_table();
+#ifndef RLE_DEC_TBL32
+#define RLE_DEC_TBL32 0
+#endif
+// packed form (1 KiB): bits 0..23 = the three masks, bits 24+2d = exit offset from entry d
+#if RLE_DEC_TBL32
+typedef u32 DecEntry;
+__device__ __forceinline__ DecEntry dec_entry_from(uint2 e) {
+    return (e.x & 0xFFFFFFu) | ((e.y & 3u) << 24) | (((e.y >> 8) & 3u) << 26) | (((e.y >> 16) & 3u) << 28);
+}
+__device__ __forceinline__ u32 ent_masks(DecEntry e) { return e; }
+__device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e, 24u + 2u * d, 2); }
+__device__ __forceinline__ u32 ent_sel(DecEntry e) {
+    const u32 x = e >> 24;
+    return (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | 0x03000000u;
+}
+#else
+typedef uint2 DecEntry;
+__device__ __forceinline__ DecEntry dec_entry_from(uint2 e) { return e; }
+__device__ __forceinline__ u32 ent_masks(DecEntry e) { return e.x; }
+__device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e.y, 8u * d, 8); }
+__device__ __forceinline__ u32 ent_sel(DecEntry e) { return e.y; }
+#endif
 
 // Staging (per wave): decoded position r (biased by 16: chunk 0 is never stored) holds a u16:
 // 0 = no token starts here, else 0x8000 | (r & 15) << 8 | byte at a token start.  Within a
@@ -386,6 +482,7 @@ struct DecState {
     u32 fillc;     // byte of the last stored position (run continuation carry)
     u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
     u32 serial;    // 1 -> stream needs the exact serial path
+    Stamps sp;     // diagnostic builds only
 };
 
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
@@ -428,9 +525,11 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
     return rounds;
 }
 
-__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u32 U, u32 lane, const uint2* tbl,
-                                        uint8_t* stage, u32 trash_addr, u32x4 rso, DecState& st) {
+__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 U, u32 lane,
+                                        const DecEntry* tbl, uint8_t* stage, u32 trash_addr, u32x4 rso, DecState& st) {
+    RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    next();   // the slot is free once read
     const u32 p0 = pos + 16u * lane;
     const u32 left = p0 < C ? C - p0 : 0u;
     const u32 nl = left < 16u ? left : 16u;
@@ -449,13 +548,14 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u3
     const u32 NE = nz4(w[0] ^ alignbyte(w[1], w[0], 1)) | (nz4(w[1] ^ alignbyte(w[2], w[1], 1)) << 4) |
                    (nz4(w[2] ^ alignbyte(w[3], w[2], 1)) << 8) | (nz4(w[3] ^ alignbyte(la, w[3], 1)) << 12);
     const u32 E = ~NE & 0xFFFFu;
-    const uint2 ta = tbl[E & 0xFFu], tb = tbl[E >> 8];
-    const u32 map = lane < kOwnLanes ? __builtin_amdgcn_perm(tb.y, tb.y, ta.y) : kMapId;
+    const DecEntry ta = tbl[E & 0xFFu], tb = tbl[E >> 8];
+    const u32 selb = ent_sel(tb);
+    const u32 map = lane < kOwnLanes ? __builtin_amdgcn_perm(selb, selb, ent_sel(ta)) : kMapId;
     const u32 incl = wave_scan_incl(map, kMapId, OpMap());
     const u32 excl = from_prev_lane(incl, kMapId);
     const u32 dl = bfe(excl, 8u * st.d, 8);
-    const u32 mid = bfe(ta.y, 8u * dl, 8);
-    const u32 S = (bfe(ta.x, 8u * dl, 8) | (bfe(tb.x, 8u * mid, 8) << 8)) & validm;
+    const u32 mid = ent_exit(ta, dl);
+    const u32 S = (bfe(ent_masks(ta), 8u * dl, 8) | (bfe(ent_masks(tb), 8u * mid, 8) << 8)) & validm;
     const u32 P = S & E;
 
     // token lengths: digit d (byte j+2) in '1'..'9' -> d-'0'; digits in the zero padding mark
@@ -472,7 +572,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u3
         const u32 mpb = nib_to_bytes(bfe(MP, 4u * k, 4));
         const u32 dor = dg[k] | 0x80808080u;
         const u32 lo = dor - 0x31313131u, hi = dor - 0x3A3A3A3Au;
-        const u32 dm1 = lo & 0x7F7F7F7Fu & (mpb * 0xFFu);   // d - '1' at pair starts
+        const u32 dm1 = lo & 0x7F7F7F7Fu & ((mpb << 8) - mpb);   // d - '1' at pair starts
         extra = __builtin_amdgcn_udot4(dm1, 0x01010101u, extra, false);
         badb |= (~lo | hi | dg[k]) & (mpb << 7);
         W[k] = nib_to_bytes(bfe(S, 4u * k, 4)) + dm1;        // decoded length per position
@@ -492,6 +592,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u3
         st.tail = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
     }
 
+    RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
     // scatter a key at each token start's decoded position; other positions write a private
     // slot.  o2 = 2 x position; odd positions store the key from the high half (d16_hi).
     const u32 rel0 = st.out_pos - st.flushed;
@@ -512,6 +613,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u3
         o2 += w2;
     }
     wave_lds_sync();
+    RLE_STAMP(st.sp, 2);   // scatter
 
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
@@ -527,6 +629,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, u32 pos, u32 C, u3
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
     st.d = bfe(readlane(incl, 63), 8u * st.d, 8);
+    RLE_STAMP(st.sp, 4);   // flush
     return rounds;
 }
 
@@ -608,30 +711,38 @@ __device__ u32 dec_serial(const uint8_t* src, u32 C, u32 U, uint64_t cap, uint8_
     return readlane(st, 0);
 }
 
-__global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint64_t* __restrict__ in_len,
-                                                        uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        const uint64_t* __restrict__ out_len,
-                                                        const uint64_t* __restrict__ out_cap,
-                                                        uint32_t* __restrict__ status, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kWavesPerBlock * 2 * kSlot];
-    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kWavesPerBlock * kDecStage];
-    __shared__ __attribute__((aligned(16))) uint16_t trash_all[kWavesPerBlock * kWave];
-    __shared__ uint2 tbl[256];
-    tbl[threadIdx.x] = dec_table_entry(threadIdx.x);
+#ifndef RLE_DEC_WAVES
+#define RLE_DEC_WAVES 4
+#endif
+// Waves per workgroup: with one, the dispatcher starts the next buffer as soon as any wave ends,
+// so short (highly compressed) and long buffers balance without a software queue.
+constexpr u32 kDecWaves = RLE_DEC_WAVES;
+constexpr u32 kDecBlock = kWave * kDecWaves;
+__global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
+                                                           const uint64_t* __restrict__ in_off,
+                                                           const uint64_t* __restrict__ in_len,
+                                                           uint8_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ out_off,
+                                                           const uint64_t* __restrict__ out_len,
+                                                           const uint64_t* __restrict__ out_cap,
+                                                           uint32_t* __restrict__ status, uint32_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kDecWaves * kDecStage];
+    __shared__ __attribute__((aligned(16))) uint16_t trash_all[kDecWaves * kWave];
+    __shared__ DecEntry tbl[256];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
+    for (u32 k = threadIdx.x; k < 256u; k += kDecBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
     uint8_t* stage = stage_all + wid * kDecStage;
-    const u32 trash_addr = lds_addr(trash_all + wid * kWave + lane);
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    const u32 trash_addr = lds_addr(trash_all + wid * kWave + lane);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
-    __syncthreads();
-    const u32 nw = gridDim.x * kWavesPerBlock;
+    if (kDecWaves > 1) __syncthreads();
+    else wave_lds_sync();
 
-    for (u32 b = blockIdx.x * kWavesPerBlock + wid; b < n; b += nw) {
+    const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
+    if (b < n) {
         const uint64_t C64 = in_len[b];
         const uint64_t U64 = out_len[b];
         const uint64_t cap = out_cap ? out_cap[b] : U64;
@@ -641,20 +752,33 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
         if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
         if (bad) {
             if (lane == 0 && status) status[b] = bad;
-            continue;
+            return;
         }
         const u32 C = (u32)C64, U = (u32)U64;
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{0u, 0u, 0u, 0u, 0u, 0u};
-        walk_tiles(rsi, ntiles_for(C), lane, slots, [&](u32 t, const uint8_t* cs) {
-            return dec_tile(cs, t * kTileStep, C, U, lane, tbl, stage, trash_addr, rso, st);
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, {}};
+#if RLE_STAMPS
+        for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
+        st.sp.last = memtime();
+        const uint64_t t_begin = st.sp.last;
+#endif
+        walk_tiles(rsi, ntiles_for(C), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+            return dec_tile(cs, nx, t * kTileStep, C, U, lane, tbl, stage, trash_addr, rso, st);
         });
+        RLE_STAMP(st.sp, 5);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
         if (st.serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
         else dec_finish(st, U, lane, stage, rso, dst);
+        RLE_STAMP(st.sp, 6);   // finish
+#if RLE_STAMPS
+        if (lane == 0) {
+            for (u32 k = 0; k < 7; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st.sp.acc[k]);
+            atomicAdd(&g_stamps[7], (unsigned long long)(st.sp.last - t_begin));
+            atomicAdd(&g_stamps[8], 1ull);
+        }
+#endif
         if (lane == 0 && status) status[b] = stat;
-        wave_lds_sync();
     }
 }
 
@@ -745,11 +869,14 @@ __global__ void selftest_kernel(uint32_t* err) {
 
 // ================================================================ C-ABI launchers
 namespace {
-inline uint32_t grid_for(uint32_t n) {
-    uint32_t blocks = (n + rle::kWavesPerBlock - 1) / rle::kWavesPerBlock;
-    if (blocks > rle::kMaxBlocks) blocks = rle::kMaxBlocks;
-    return blocks ? blocks : 1u;
+constexpr uint32_t kMaxGrid = 1u << 30;
+// one buffer per wave, kWaves waves per workgroup, rounded up to whole rounds of the 8 XCDs
+// (rle::xcd_buffer); the kernels have no grid-stride loop, so n is bounded (kMaxGrid)
+inline uint32_t grid_for(uint32_t n, uint32_t waves) {
+    const uint32_t g = (n + waves - 1) / waves;
+    return (g + rle::kXcds - 1) / rle::kXcds * rle::kXcds;
 }
+
 }  // namespace
 
 extern "C" size_t rle_max_compressed_size(size_t U) { return U + U / 2; }
@@ -759,7 +886,8 @@ extern "C" int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_of
                                        uint32_t* d_status, uint32_t n, void* stream) {
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
-    hipLaunchKernelGGL(rle::encode_kernel, dim3(grid_for(n)), dim3(rle::kBlock), 0, (hipStream_t)stream,
+    if (n > kMaxGrid) return RLE_E_INVAL;
+    hipLaunchKernelGGL(rle::encode_kernel, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
@@ -769,7 +897,8 @@ extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_of
                                        const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n, void* stream) {
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
-    hipLaunchKernelGGL(rle::decode_kernel, dim3(grid_for(n)), dim3(rle::kBlock), 0, (hipStream_t)stream,
+    if (n > kMaxGrid) return RLE_E_INVAL;
+    hipLaunchKernelGGL(rle::decode_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
                        d_status, n);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
@@ -794,6 +923,22 @@ extern "C" int rle_mi355x_selftest(void) {
     (void)hipFree(d);
     if (e1 != hipSuccess) return RLE_E_HIP;
     return (int)h;
+}
+
+extern "C" int rle_mi355x_stamps(unsigned long long* out, int reset) {
+#if RLE_STAMPS
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(rle::g_stamps), sizeof(rle::g_stamps)) != hipSuccess)
+        return RLE_E_HIP;
+    if (reset) {
+        unsigned long long z[rle::kStampSegs + 1] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rle::g_stamps), z, sizeof(z)) != hipSuccess) return RLE_E_HIP;
+    }
+    return RLE_OK;
+#else
+    (void)out;
+    (void)reset;
+    return RLE_E_INVAL;   // not a diagnostic build
+#endif
 }
 
 extern "C" int rle_mi355x_device_count(void) {

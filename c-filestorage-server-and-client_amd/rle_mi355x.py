@@ -14,6 +14,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librle_mi355x.so")
+# A/B experiments only (tools/ab.sh): load an experimental build instead of the product library
+LIB_PATH = os.environ.get("RLE_MI355X_LIB", LIB_PATH)
 INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
 
 RLE_OK = 0

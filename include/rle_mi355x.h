@@ -81,6 +81,10 @@ int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
 /* Runs the cross-lane (DPP) primitive self-test on the current device; 0 = pass. */
 int rle_mi355x_selftest(void);
 
+/* Diagnostic builds only (RLE_STAMPS=1, never the product library): per-segment decode cycle sums
+ * [wait, scan, phase A, phase B, flush, drain, finish, total, waves]; RLE_E_INVAL otherwise. */
+int rle_mi355x_stamps(unsigned long long* out9, int reset);
+
 /* Number of visible HIP devices (0 when none). */
 int rle_mi355x_device_count(void);
 
