@@ -217,7 +217,7 @@ __device__ __forceinline__ u32 pkmax(u32 a, u32 b) {
 #endif
 #if RLE_STAMPS
 constexpr u32 kStampSegs = 8;
-__device__ unsigned long long g_stamps[kStampSegs + 1];
+__device__ unsigned long long g_stamps[kStampSegs + 1];   // 8 segment sums, waves
 struct Stamps {
     uint64_t acc[kStampSegs];
     uint64_t last;
@@ -252,10 +252,12 @@ struct EncState {
     u32 flushed;    // compressed bytes already stored (multiple of 16); staging chunk 1 = flushed
     u32 prev_top;   // input byte at tile_pos-1, in bits 24..31
     u32 rs;         // start position of the run holding input byte tile_pos-1
+    Stamps sp;      // diagnostic builds only
 };
 
 __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 U, u32 lane,
                                         uint8_t* stage, u32x4 rso, EncState& st) {
+    RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
     next();   // the slot is free once read
@@ -295,6 +297,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     const u32 ttot = readlane(oincl, 63);
     const u32 rel0 = st.out_pos - st.flushed;   // 0..15: bytes of the partial chunk
 
+    RLE_STAMP(st.sp, 1);   // boundaries, run phase, token masks, offsets
     // pass 1: every position writes its byte.  A start writes at its token's offset; a valid
     // non-start (inside a 3-byte token) writes the same byte at offset-2 of the NEXT token,
     // i.e. its own token's second byte (a redundant, identical write); positions past U write
@@ -314,6 +317,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
         *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
         o += (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
     }
+    RLE_STAMP(st.sp, 2);   // pass 1
     // pass 2: second byte and count digit of each 3-byte token, written from the token's own
     // tile (its second input byte may sit in the next tile, after this tile's flush)
     u32 prem = P;
@@ -330,6 +334,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
         }
     }
     wave_lds_sync();
+    RLE_STAMP(st.sp, 3);   // pass 2
 
     // store the completed 16-byte chunks (staging chunks 1..nfl), then move the partial one
     const u32 newrel = rel0 + ttot;
@@ -341,6 +346,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
         if (c < nfl) v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
         vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, v);
     }
+    RLE_STAMP(st.sp, 4);   // flush
     if (nfl && lane < 4u) {
         u32* s32 = reinterpret_cast<u32*>(stage);
         s32[4u + lane] = s32[4u * (nfl + 1u) + lane];
@@ -351,6 +357,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     st.prev_top = readlane(top, kOwnLanes - 1u);
     const u32 i63 = readlane(incl, 63);
     st.rs = i63 > st.rs ? i63 : st.rs;
+    RLE_STAMP(st.sp, 5);   // partial-chunk move, state
     return rounds;
 }
 
@@ -406,16 +413,28 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     const u32 U = (u32)U64;
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
-    EncState st{0u, 0u, 0u, 0u};
+    EncState st{0u, 0u, 0u, 0u, {}};
+#if RLE_STAMPS
+    for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
+    st.sp.last = memtime();
+#endif
     walk_tiles(rsi, ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         return enc_tile(cs, nx, t * kTileStep, U, lane, stage, rso, st);
     });
+    RLE_STAMP(st.sp, 6);   // drain
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
     if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
     if (lane == 0) {
         out_len[b] = st.out_pos;
         if (status) status[b] = RLE_STATUS_OK;
     }
+    RLE_STAMP(st.sp, 7);   // finish
+#if RLE_STAMPS
+    if (lane == 0) {
+        for (u32 k = 0; k < kStampSegs; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st.sp.acc[k]);
+        atomicAdd(&g_stamps[kStampSegs], 1ull);
+    }
+#endif
 }
 
 // ================================================================ DECODE
@@ -486,7 +505,8 @@ struct DecState {
 };
 
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
-__device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc) {
+__device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
+                                         Stamps& sp) {
     const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
@@ -497,6 +517,7 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
 #pragma unroll
             for (u32 m = 0; m < 8; ++m) L[m] = s32[m];
         }
+        RLE_STAMP(sp, 3);   // flush: staging reads
         // prefix max of the keys inside the chunk: within each pair, then across pairs
 #pragma unroll
         for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
@@ -513,7 +534,9 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
         o.z = __builtin_amdgcn_perm(pkmax(L[5], crep), pkmax(L[4], crep), 0x06040200u);
         o.w = __builtin_amdgcn_perm(pkmax(L[7], crep), pkmax(L[6], crep), 0x06040200u);
+        RLE_STAMP(sp, 4);   // flush: fill + carry scan
         vstore(rso, active ? flushed + 16u * c : kOOB, o);
+        RLE_STAMP(sp, 5);   // flush: store issue
         if (active) {
 #pragma unroll
             for (u32 m = 0; m < 8; ++m) s32[m] = 0u;
@@ -521,6 +544,7 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
         fillc = readlane(o.w >> 24, lastlane);
         wave_lds_sync();
+        RLE_STAMP(sp, 6);   // flush: re-zero + sync
     }
     return rounds;
 }
@@ -617,7 +641,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
 
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
-    const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc);
+    const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc, st.sp);
     if (nfl) {   // move the partial chunk to staging chunk 1
         if (lane < 8u) {
             u32* s32 = reinterpret_cast<u32*>(stage);
@@ -629,7 +653,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
     st.d = bfe(readlane(incl, 63), 8u * st.d, 8);
-    RLE_STAMP(st.sp, 4);   // flush
+    RLE_STAMP(st.sp, 7);   // partial-chunk move, state
     return rounds;
 }
 
@@ -761,21 +785,19 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
         st.sp.last = memtime();
-        const uint64_t t_begin = st.sp.last;
 #endif
         walk_tiles(rsi, ntiles_for(C), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
             return dec_tile(cs, nx, t * kTileStep, C, U, lane, tbl, stage, trash_addr, rso, st);
         });
-        RLE_STAMP(st.sp, 5);   // drain after the last tile
+        RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
         if (st.serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
         else dec_finish(st, U, lane, stage, rso, dst);
-        RLE_STAMP(st.sp, 6);   // finish
+        RLE_STAMP(st.sp, 7);   // finish
 #if RLE_STAMPS
         if (lane == 0) {
-            for (u32 k = 0; k < 7; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st.sp.acc[k]);
-            atomicAdd(&g_stamps[7], (unsigned long long)(st.sp.last - t_begin));
-            atomicAdd(&g_stamps[8], 1ull);
+            for (u32 k = 0; k < kStampSegs; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st.sp.acc[k]);
+            atomicAdd(&g_stamps[kStampSegs], 1ull);
         }
 #endif
         if (lane == 0 && status) status[b] = stat;

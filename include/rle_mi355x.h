@@ -82,7 +82,8 @@ int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
 int rle_mi355x_selftest(void);
 
 /* Diagnostic builds only (RLE_STAMPS=1, never the product library): per-segment decode cycle sums
- * [wait, scan, phase A, phase B, flush, drain, finish, total, waves]; RLE_E_INVAL otherwise. */
+ * over all waves: [tile wait, scan, scatter, flush reads, flush fill, flush store, flush re-zero,
+ * move/drain/finish, waves]; RLE_E_INVAL otherwise. */
 int rle_mi355x_stamps(unsigned long long* out9, int reset);
 
 /* Number of visible HIP devices (0 when none). */
