@@ -67,6 +67,8 @@ WORKLOADS = {
     "k64_random": dict(n=16384, size=65536, kinds=(1,), ref_kinds="1", desc="16384 x 64 KiB random"),
     "k64_runs50": dict(n=16384, size=65536, kinds=(2,), ref_kinds="2", desc="16384 x 64 KiB runs50"),
     "k64_runs90": dict(n=16384, size=65536, kinds=(3,), ref_kinds="3", desc="16384 x 64 KiB runs90"),
+    "one4m": dict(n=1, size=4 << 20, kinds=(1,), ref_kinds="1", desc="1 x 4 MiB random (one large file)"),
+    "one64m": dict(n=1, size=64 << 20, kinds=(2,), ref_kinds="2", desc="1 x 64 MiB runs50 (one large file)"),
     "mixed": dict(n=1024, size=None, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
                   desc="configs[2]: 1024 mixed 4 KiB-1 MiB buffers per GPU (zero / random / runs50 / runs90)"),
     "cfg3": dict(n=131072, size=65536, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
@@ -84,6 +86,9 @@ class Batch:
         sizes = [wl["size"] if wl["size"] else mixed_size(i) for i in gidx]
         offs, total = R.layout(sizes)
         coffs, ctotal = R.compressed_slots(sizes)
+        self.c_cap = ctotal
+        self.ws_enc = R.seg_workspace(n, sum(sizes), dev)
+        self.ws_dec = R.seg_workspace(n, ctotal, dev)
         i64 = lambda v: torch.tensor(v, dtype=torch.int64, device=dev)
         self.n = n
         self.sizes = sizes
@@ -99,12 +104,23 @@ class Batch:
         R.gen_synthetic(self.d_in, self.offs, self.lens, kind_t, i64(gidx))
         torch.cuda.synchronize()
 
+    seg = False   # True: the segmented (several waves per buffer) entry points
+
     def encode(self, stream=None):
-        R.encode_batch(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status, stream=stream)
+        if self.seg:
+            R.encode_batch_seg(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status,
+                               total_in_bytes=self.u_bytes, workspace=self.ws_enc, stream=stream)
+        else:
+            R.encode_batch(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status,
+                           stream=stream)
 
     def decode(self, stream=None):
-        R.decode_batch(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
-                       stream=stream)
+        if self.seg:
+            R.decode_batch_seg(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
+                               total_in_bytes=self.c_cap, workspace=self.ws_dec, stream=stream)
+        else:
+            R.decode_batch(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
+                           stream=stream)
 
 
 def time_kernels(fn, reps, stream):

@@ -1,0 +1,746 @@
+// rle_device.h — device-side building blocks of the MI355X (gfx950) RLE codec, shared by the
+// one-wave-per-buffer batch kernels (rle_kernels.hip) and the multi-wave segmented kernels
+// (rle_segmented.hip): cross-lane primitives, the hand-counted LDS-DMA tile pipeline, and the
+// encode / decode tile steps (reference src/rleCompression.c:9-62; grammar in SURVEY.md App. A).
+#pragma once
+//
+// Device-resident forms of the reference codec (samul-1/C-FileStorage-Server-and-Client
+// src/rleCompression.c:9-62; grammar restated in SURVEY.md Appendix A):
+//   encode: maximal runs cut into 9-byte chunks; a chunk of r bytes of v emits "v" (r == 1)
+//           or "v v ('0'+r)" (r >= 2)                          — src/rleCompression.c:13-41
+//   decode: token at j emits y[j]; when y[j] == y[j+1] the token is 3 bytes and adds
+//           (signed char)y[j+2]-'0'-1 copies, capped at U      — src/rleCompression.c:50-60
+//
+// Execution model: a wave64 walks its buffer (or segment) in 1 KiB tiles, 16 bytes
+// per lane.  Loads are range-checked LDS-DMA buffer_load_dwordx4 (two slots, two tiles in flight);
+// their completion is counted by hand (s_waitcnt vmcnt(N), N = the memory ops issued since),
+// because hipcc's own bookkeeping drains the queue at every loop header once a variable number of
+// stores sits in the loop.  Run boundaries and token starts are 16-bit per-lane masks from SWAR
+// byte compares; the sequential state (encode: run start position; decode: token phase 0..2 as a
+// v_perm byte map) and output offsets cross lanes by DPP wave scans and cross tiles in scalar
+// registers.  Each lane scatters its output into a per-wave LDS staging area that is linear per
+// tile, and complete 16-byte chunks leave as coalesced buffer_store_dwordx4.  No MFMA: this is an
+// HBM-bound byte scan.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rle_mi355x.h"
+
+namespace rle {
+
+typedef uint32_t u32;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr u32 kWave = 64;
+constexpr u32 kMaxBufferBytes = 0x7FFFFFF0u;   // per-buffer limit (32-bit in-buffer offsets)
+constexpr u32 kOOB = 0x80000000u;               // store offset dropped by the range check
+
+// ---------------------------------------------------------------- cross-lane primitives (DPP)
+enum : int {
+    kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118,
+    kRowBcast15 = 0x142, kRowBcast31 = 0x143, kWaveShl1 = 0x130, kWaveShr1 = 0x138,
+};
+
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ u32 dpp(u32 old, u32 src) {
+    return (u32)__builtin_amdgcn_update_dpp((int)old, (int)src, kCtrl, kRowMask, 0xf, false);
+}
+// value of lane-1 (lane 0 gets `fill`) / of lane+1 (lane 63 gets `fill`)
+__device__ __forceinline__ u32 from_prev_lane(u32 v, u32 fill) { return dpp<kWaveShr1>(fill, v); }
+__device__ __forceinline__ u32 from_next_lane(u32 v, u32 fill) { return dpp<kWaveShl1>(fill, v); }
+__device__ __forceinline__ u32 readlane(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
+__device__ __forceinline__ u32 uniform(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Inclusive wave scan for an associative op(a_earlier, b_later) with identity `id`.
+// Must be called with all 64 lanes active.
+template <class Op>
+__device__ __forceinline__ u32 wave_scan_incl(u32 x, u32 id, Op op) {
+    x = op(dpp<kRowShr1>(id, x), x);
+    x = op(dpp<kRowShr2>(id, x), x);
+    x = op(dpp<kRowShr4>(id, x), x);
+    x = op(dpp<kRowShr8>(id, x), x);
+    x = op(dpp<kRowBcast15, 0xa>(id, x), x);
+    x = op(dpp<kRowBcast31, 0xc>(id, x), x);
+    return x;
+}
+struct OpAdd {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return a + b; }
+};
+struct OpMax {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return a > b ? a : b; }
+};
+// "latest present value": values are 0 (absent) or 0x100|byte
+struct OpLatest {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return b ? b : a; }
+};
+// token-phase maps {0,1,2} -> {0,1,2} as v_perm selectors: byte d = image of d; byte 3 = 3
+constexpr u32 kMapId = 0x03020100u;
+struct OpMap {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const { return __builtin_amdgcn_perm(b, b, a); }
+};
+// encode phase transfer functions (self-test only): code >= 16 -> constant, else add mod 9
+__device__ __forceinline__ u32 mod9s(u32 x) { return x >= 9u ? x - 9u : x; }
+struct OpPhase9 {
+    __device__ __forceinline__ u32 operator()(u32 a, u32 b) const {
+        return b >= 16u ? b : (a >= 16u ? 16u + mod9s(a - 16u + b) : mod9s(a + b));
+    }
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------- byte SWAR helpers
+// bit k (k = 0..3) set iff byte k of d is non-zero
+__device__ __forceinline__ u32 nz4(u32 d) {
+    u32 t = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+    t >>= 7;             // bytes' flags at bits 0, 8, 16, 24
+    t |= t >> 7;         // ... at bits 0, 1 and 16, 17
+    return (t | (t >> 14)) & 0xFu;
+}
+// byte 0 of x in all four bytes (v_perm: selector bytes 0..3 pick bytes of the second operand)
+__device__ __forceinline__ u32 rep4(u32 x) { return __builtin_amdgcn_perm(0u, x, 0u); }
+__device__ __forceinline__ u32 lowmask(u32 nbits) { return nbits >= 32u ? ~0u : ((1u << nbits) - 1u); }
+__device__ __forceinline__ u32 alignbyte(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
+__device__ __forceinline__ u32 bfe(u32 v, u32 off, u32 w) { return __builtin_amdgcn_ubfe(v, off, w); }
+__device__ __forceinline__ u32 bcnt(u32 v, u32 acc) { return (u32)__builtin_popcount(v) + acc; }
+// 4-bit mask -> bytes 0x01
+__device__ __forceinline__ u32 nib_to_bytes(u32 n) { return (n * 0x00204081u) & 0x01010101u; }
+__device__ __forceinline__ u32 mod9(u32 x) {
+    const u32 q = __umulhi(x, 0x38E38E39u) >> 1;
+    return x - 9u * q;
+}
+
+// ---------------------------------------------------------------- memory pipeline (hand-counted)
+// 128-bit buffer resource (raw buffer, stride 0): loads past num_records return 0, stores past
+// it are dropped.  Built from wave-uniform values only.
+__device__ __forceinline__ u32x4 make_rsrc(const void* base, u32 nbytes) {
+    const uint64_t a = (uint64_t)base;
+    u32x4 r;
+    r.x = (u32)a;
+    r.y = (u32)(a >> 32) & 0xFFFFu;
+    r.z = nbytes;
+    r.w = 0x00020000u;
+    return r;
+}
+// LDS byte address of a __shared__ pointer
+__device__ __forceinline__ u32 lds_addr(const void* p) {
+    return (u32)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// Loads and stores in asm: hipcc neither counts nor waits for them; vm_wait() is the only wait
+// for them.  Loads go straight to LDS (LDS-DMA: lane i's 16 bytes land at lds + 16 i), so no
+// VGPR is in flight that the compiler could copy or reuse before the data lands.
+__device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
+    u32 keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"   // earlier ds_reads of this slot have completed
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(lds), "s"(rs)
+        : "memory");
+}
+#ifndef RLE_NOSTORE
+#define RLE_NOSTORE 0
+#endif
+__device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v) {
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+// wait until at most n vector-memory ops are outstanding
+#define RLE_VMW(N)                                            \
+    case N:                                                   \
+        asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+        break;
+__device__ __forceinline__ void vm_wait(u32 n) {
+    switch (n < 15u ? n : 15u) {
+        RLE_VMW(0) RLE_VMW(1) RLE_VMW(2) RLE_VMW(3) RLE_VMW(4) RLE_VMW(5) RLE_VMW(6) RLE_VMW(7) RLE_VMW(8)
+        RLE_VMW(9) RLE_VMW(10) RLE_VMW(11) RLE_VMW(12) RLE_VMW(13) RLE_VMW(14) RLE_VMW(15)
+        default: break;
+    }
+}
+#undef RLE_VMW
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Tiles overlap: tile t is input [1008 t, 1008 t + 1024); lanes 0..62 own its first 1008 bytes
+// and lane 63 holds the next tile's first 16 bytes (the lookahead of lane 62).  Each tile is one
+// LDS-DMA into one of two slots.  A step reads its slot once (one ds_read_b128 per lane) and then
+// calls next() to refill that slot with tile t+2, so two tiles are in flight behind the one being
+// processed.  step(t, slot, next) returns the store instructions it issued after next() (or ~0u to
+// stop).  Vector-memory ops complete in issue order, so the wait for tile t+1 (issued inside step
+// t-1, before that step's stores) leaves step t-1's stores, the refill and step t's stores in
+// flight.  Loads past the buffer (t+2 >= ntiles) are range-checked to zero and cost no traffic.
+constexpr u32 kOwnLanes = 63;
+constexpr u32 kTileStep = 16 * kOwnLanes;   // 1008
+constexpr u32 kSlot = 16 * kWave;           // 1024
+struct Refill {
+    u32x4 rs;
+    u32 voff;   // lane byte offset of tile t+2
+    u32 lds;    // slot LDS address
+    __device__ __forceinline__ void operator()() const { dma_tile(rs, voff, lds); }
+};
+// Tiles start at `start` (bytes from the buffer descriptor's base): tile t is [start + 1008 t, ...).
+template <class Step>
+__device__ __forceinline__ void walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots,
+                                           Step step) {
+    const u32 lo = start + 16u * lane;
+    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
+    dma_tile(rs, lo, l0);
+    dma_tile(rs, kTileStep + lo, l1);
+    u32 p1 = 0, p2 = 0;   // stores of the last step and of the one before
+    for (u32 t = 0; t < ntiles; t += 2) {
+        vm_wait(p2 + 1u + p1);
+        p2 = p1;
+        p1 = step(t, slots, Refill{rs, (t + 2u) * kTileStep + lo, l0});
+        if (p1 == ~0u || t + 1u >= ntiles) break;
+        vm_wait(p2 + 1u + p1);
+        p2 = p1;
+        p1 = step(t + 1u, slots + kSlot, Refill{rs, (t + 3u) * kTileStep + lo, l1});
+        if (p1 == ~0u) break;
+    }
+    vm_drain();
+}
+__device__ __forceinline__ u32 ntiles_for(u32 n) { return (n + kTileStep - 1u) / kTileStep; }
+
+// packed u16 max
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32 pkmax(u32 a, u32 b) {
+    return __builtin_bit_cast(u32, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+}
+
+// ---------------------------------------------------------------- diagnostic stamps
+// RLE_STAMPS=1 builds (never the product library) sum s_memtime cycles per decode segment in
+// each wave and add them into g_stamps; rle_mi355x_stamps() reads the sums.  Read shares only:
+// each stamp drains the LDS queue (MI355X guide, "In-kernel stamps").
+#ifndef RLE_STAMPS
+#define RLE_STAMPS 0
+#endif
+#if RLE_STAMPS
+constexpr u32 kStampSegs = 8;
+static __device__ unsigned long long g_stamps[kStampSegs + 1];   // 8 segment sums, waves
+struct Stamps {
+    uint64_t acc[kStampSegs];
+    uint64_t last;
+};
+__device__ __forceinline__ uint64_t memtime() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define RLE_STAMP(SP, I)                  \
+    do {                                  \
+        const uint64_t _t = memtime();    \
+        (SP).acc[I] += _t - (SP).last;    \
+        (SP).last = _t;                   \
+    } while (0)
+#else
+struct Stamps {};
+#define RLE_STAMP(SP, I) \
+    do {                 \
+    } while (0)
+#endif
+
+// ================================================================ ENCODE
+// Staging (per wave): output position r of the tile (biased by 16: chunk 0 is a guard for the
+// back-writes of non-starts) lives at byte r.
+constexpr u32 kEncStage = 2048;   // >= 16 + 15 + 1512 + 2
+
+struct EncState {
+    u32 out_pos;    // compressed bytes produced so far
+    u32 flushed;    // compressed bytes already stored (multiple of 16); staging chunk 1 = flushed
+    u32 prev_top;   // input byte at tile_pos-1, in bits 24..31
+    u32 rs;         // start position of the run holding input byte tile_pos-1
+    u32 head;       // leading bytes of the first stored chunk that belong to the previous segment
+    Stamps sp;      // diagnostic builds only
+};
+
+// Positions are absolute in the buffer.  Tokens start only below Uo (the end of the positions this
+// wave owns: the buffer, or its segment); runs end at Ud (the buffer's end).
+// Analysis of one encode tile (shared by enc_tile and the segment summary): per lane, the run
+// boundary mask B (+ the next lane's 8 bits in B24), token starts T and 3-byte tokens P, and the
+// wave max-scan of the last boundary position.
+struct EncAn {
+    u32 w[4];
+    u32 p0, validm, top, B, B24, incl, T, P;
+};
+__device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u32 Uo, u32 lane, u32 prev_top,
+                                             u32 rs) {
+    EncAn a;
+    a.w[0] = cur.x; a.w[1] = cur.y; a.w[2] = cur.z; a.w[3] = cur.w;
+    const u32* w = a.w;
+    const u32 p0 = pos + 16u * lane;
+    a.p0 = p0;
+    const u32 left = p0 < Ud ? Ud - p0 : 0u;
+    const u32 nl = left < 16u ? left : 16u;
+    const u32 lefto = p0 < Uo ? Uo - p0 : 0u;
+    const u32 validm = lane < kOwnLanes ? lowmask(lefto < 16u ? lefto : 16u) : 0u;   // lane 63: lookahead only
+    a.validm = validm;
+
+    // run boundaries: bit j <=> x[p0+j] != x[p0+j-1] (or p0+j == 0); positions >= Ud end runs
+    const u32 top = w[3] & 0xFF000000u;
+    a.top = top;
+    const u32 ptop = from_prev_lane(top, prev_top);
+    u32 B = nz4(w[0] ^ alignbyte(w[0], ptop, 3)) | (nz4(w[1] ^ alignbyte(w[1], w[0], 3)) << 4) |
+            (nz4(w[2] ^ alignbyte(w[2], w[1], 3)) << 8) | (nz4(w[3] ^ alignbyte(w[3], w[2], 3)) << 12);
+    B |= (p0 == 0u) ? 1u : 0u;
+    B |= ~lowmask(nl) & 0xFFFFu;
+    a.B = B;
+    a.B24 = B | ((from_next_lane(B, 0xFFu) & 0xFFu) << 16);   // + next 8 bytes (repeat lookahead)
+
+    // run start of byte p0-1: max-scan of the last boundary position per owning lane
+    const u32 lbp = (B && lane < kOwnLanes) ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
+    const u32 incl = wave_scan_incl(lbp, 0u, OpMax());
+    a.incl = incl;
+    const u32 pm = from_prev_lane(incl, 0u);
+    const u32 rsl = pm > rs ? pm : rs;
+    const u32 qin = mod9(p0 - 1u - rsl);   // run phase of byte p0-1 (unused when p0 starts a run)
+
+    // token starts: run starts, 9 past a run start, and the continuation of the run entering
+    const u32 f1 = (u32)__builtin_ctz(B | 0x10000u);
+    u32 t8 = B | (B << 1);
+    t8 |= t8 << 2;
+    t8 |= t8 << 4;
+    t8 |= B << 8;
+    const u32 pre = (0x201u << (8u - qin)) & lowmask(f1);
+    a.T = (B | ((B << 9) & ~t8) | pre) & validm;
+    a.P = a.T & ~(a.B24 >> 1);   // 3-byte tokens: the run continues past the start
+    return a;
+}
+
+__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
+                                        u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st) {
+    RLE_STAMP(st.sp, 0);   // DMA wait + loop
+    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    next();   // the slot is free once read
+    const EncAn an = enc_analyze(cur, pos, Ud, Uo, lane, st.prev_top, st.rs);
+    const u32* w = an.w;
+    const u32 validm = an.validm, top = an.top, B24 = an.B24, incl = an.incl, T = an.T, P = an.P;
+
+    const u32 nout = bcnt(P, bcnt(P, bcnt(T, 0u)));
+    const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, 63);
+    const u32 rel0 = st.out_pos - st.flushed;   // 0..15: bytes of the partial chunk
+
+    RLE_STAMP(st.sp, 1);   // boundaries, run phase, token masks, offsets
+    // pass 1: every position writes its byte.  A start writes at its token's offset; a valid
+    // non-start (inside a 3-byte token) writes the same byte at offset-2 of the NEXT token,
+    // i.e. its own token's second byte (a redundant, identical write); positions past U write
+    // at the tile's output end, which is never stored.  Per-position weights (T + 2P) and
+    // back-offsets (2 for valid non-starts) are byte vectors.
+    const u32 NS = validm & ~T;
+    u32 W[4], D[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        W[k] = nib_to_bytes(bfe(T, 4u * k, 4)) + 2u * nib_to_bytes(bfe(P, 4u * k, 4));
+        D[k] = 2u * nib_to_bytes(bfe(NS, 4u * k, 4));
+    }
+    u32 o = lds_addr(stage) + 16u + rel0 + oincl - nout;   // LDS byte address of the lane's output
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 a = o - ((D[j >> 2] >> (8u * (j & 3u))) & 0xFFu);
+        *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
+        o += (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+    }
+    RLE_STAMP(st.sp, 2);   // pass 1
+    // pass 2: second byte and count digit of each 3-byte token, written from the token's own
+    // tile (its second input byte may sit in the next tile, after this tile's flush)
+    u32 prem = P;
+    while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
+        if (prem) {
+            const u32 j = (u32)__builtin_ctz(prem);
+            prem &= prem - 1u;
+            const u32 mj = lowmask(j);
+            const u32 oj = 16u + rel0 + oincl - nout + bcnt(T & mj, 0u) + 2u * bcnt(P & mj, 0u);
+            const u32 rem = (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u) + 1u;   // min(9, run left)
+            const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
+            stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
+            stage[oj + 2u] = (uint8_t)('0' + rem);
+        }
+    }
+    wave_lds_sync();
+    RLE_STAMP(st.sp, 3);   // pass 2
+
+    // store the completed 16-byte chunks (staging chunks 1..nfl), then move the partial one
+    const u32 newrel = rel0 + ttot;
+    const u32 nfl = newrel >> 4;
+    const u32 rounds = (nfl + kWave - 1u) / kWave;
+    for (u32 k = 0; k < rounds; ++k) {
+        const u32 c = k * kWave + lane;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (c < nfl) v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
+        const bool skip = st.head && c == 0u;   // shared with the previous segment: byte stores below
+        vstore(rso, (c < nfl && !skip) ? st.flushed + 16u * c : kOOB, v);
+        if (skip && nfl) {
+            const u32 wv[4] = {v.x, v.y, v.z, v.w};
+            for (u32 j = st.head; j < 16u; ++j) dst[st.flushed + j] = (uint8_t)(wv[j >> 2] >> (8u * (j & 3u)));
+        }
+    }
+    if (nfl) st.head = 0;
+    RLE_STAMP(st.sp, 4);   // flush
+    if (nfl && lane < 4u) {
+        u32* s32 = reinterpret_cast<u32*>(stage);
+        s32[4u + lane] = s32[4u * (nfl + 1u) + lane];
+    }
+    wave_lds_sync();
+    st.flushed += 16u * nfl;
+    st.out_pos += ttot;
+    st.prev_top = readlane(top, kOwnLanes - 1u);
+    const u32 i63 = readlane(incl, 63);
+    st.rs = i63 > st.rs ? i63 : st.rs;
+    RLE_STAMP(st.sp, 5);   // partial-chunk move, state
+    return rounds;
+}
+
+// ================================================================ DECODE
+// Token-phase table: for an 8-bit mask e of "byte j equals byte j+1" and entry offset d (the
+// first token start in the group, 0..2): .x byte d = token-start mask, .y byte d = offset of the
+// first start past the group (.y byte 3 = 3, so .y is a v_perm selector).
+struct DecTable {
+    uint2 e[256];
+};
+constexpr DecTable make_dec_table() {
+    DecTable t{};
+    for (u32 e = 0; e < 256; ++e) {
+        u32 masks = 0, exits = 3u << 24;
+        for (u32 d = 0; d < 3; ++d) {
+            u32 s = d, m = 0;
+            while (s < 8) {
+                m |= 1u << s;
+                s += ((e >> s) & 1u) ? 3u : 1u;
+            }
+            masks |= m << (8u * d);
+            exits |= (s - 8u) << (8u * d);
+        }
+        t.e[e].x = masks;
+        t.e[e].y = exits;
+    }
+    return t;
+}
+static __constant__ DecTable kDecTable = make_dec_table();
+#ifndef RLE_DEC_TBL32
+#define RLE_DEC_TBL32 0
+#endif
+// packed form (1 KiB): bits 0..23 = the three masks, bits 24+2d = exit offset from entry d
+#if RLE_DEC_TBL32
+typedef u32 DecEntry;
+__device__ __forceinline__ DecEntry dec_entry_from(uint2 e) {
+    return (e.x & 0xFFFFFFu) | ((e.y & 3u) << 24) | (((e.y >> 8) & 3u) << 26) | (((e.y >> 16) & 3u) << 28);
+}
+__device__ __forceinline__ u32 ent_masks(DecEntry e) { return e; }
+__device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e, 24u + 2u * d, 2); }
+__device__ __forceinline__ u32 ent_sel(DecEntry e) {
+    const u32 x = e >> 24;
+    return (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | 0x03000000u;
+}
+#else
+typedef uint2 DecEntry;
+__device__ __forceinline__ DecEntry dec_entry_from(uint2 e) { return e; }
+__device__ __forceinline__ u32 ent_masks(DecEntry e) { return e.x; }
+__device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e.y, 8u * d, 8); }
+__device__ __forceinline__ u32 ent_sel(DecEntry e) { return e.y; }
+#endif
+
+// Staging (per wave): decoded position r (biased by 16: chunk 0 is never stored) holds a u16:
+// 0 = no token starts here, else 0x8000 | (r & 15) << 8 | byte at a token start.  Within a
+// 16-aligned chunk the keys grow with position (and survive moving the chunk), so a packed-u16
+// prefix max fills each run from its start.  Chunks sit at a 36-byte stride (16 x 2 B + 4 B pad) against bank conflicts.
+constexpr u32 kDecChunks = 192;              // >= ceil((16 + 15 + 3024 + 1) / 16)
+constexpr u32 kDecStage = 36u * kDecChunks;  // bytes per wave
+__device__ __forceinline__ u32 dpad(u32 r) { return 2u * r + ((r >> 4) << 2); }
+
+struct DecState {
+    u32 out_pos;   // decoded bytes produced so far
+    u32 flushed;   // decoded bytes already stored (multiple of 16); staging chunk 1 = flushed
+    u32 d;         // offset of the first token start in the current tile (0..2)
+    u32 fillc;     // byte of the last stored position (run continuation carry)
+    u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
+    u32 serial;    // 1 -> stream needs the exact serial path
+    u32 head;      // leading bytes of the first stored chunk that belong to the previous segment
+    Stamps sp;     // diagnostic builds only
+};
+
+// Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
+__device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
+                                         u32& head, uint8_t* dst, Stamps& sp) {
+    const u32 rounds = (nfl + kWave - 1u) / kWave;
+    for (u32 k = 0; k < rounds; ++k) {
+        const u32 c = k * kWave + lane;
+        const bool active = c < nfl;
+        u32* s32 = reinterpret_cast<u32*>(stage + 36u * (c + 1u));
+        u32 L[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        if (active) {
+#pragma unroll
+            for (u32 m = 0; m < 8; ++m) L[m] = s32[m];
+        }
+        RLE_STAMP(sp, 3);   // flush: staging reads
+        // prefix max of the keys inside the chunk: within each pair, then across pairs
+#pragma unroll
+        for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
+#pragma unroll
+        for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m - 1], L[m - 1], 0x03020302u));
+        const u32 lastk = L[7] >> 16;
+        const u32 lv = (lastk & 0x8000u) ? (0x100u | (lastk & 0xFFu)) : 0u;
+        const u32 incl = wave_scan_incl(lv, 0u, OpLatest());
+        const u32 before = from_prev_lane(incl, 0u);
+        const u32 carry = (before ? before : fillc) & 0xFFu;
+        const u32 crep = carry * 0x00010001u;
+        u32x4 o;
+        o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
+        o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
+        o.z = __builtin_amdgcn_perm(pkmax(L[5], crep), pkmax(L[4], crep), 0x06040200u);
+        o.w = __builtin_amdgcn_perm(pkmax(L[7], crep), pkmax(L[6], crep), 0x06040200u);
+        RLE_STAMP(sp, 4);   // flush: fill + carry scan
+        const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
+        vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o);   // RLE_NOSTORE: diagnostic
+        if (skip && active) {
+            const u32 wv[4] = {o.x, o.y, o.z, o.w};
+            for (u32 j = head; j < 16u; ++j) dst[flushed + j] = (uint8_t)(wv[j >> 2] >> (8u * (j & 3u)));
+        }
+        head = 0;
+        RLE_STAMP(sp, 5);   // flush: store issue
+        if (active) {
+#pragma unroll
+            for (u32 m = 0; m < 8; ++m) s32[m] = 0u;
+        }
+        const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
+        fillc = readlane(o.w >> 24, lastlane);
+        wave_lds_sync();
+        RLE_STAMP(sp, 6);   // flush: re-zero + sync
+    }
+    return rounds;
+}
+
+// Decode tile analysis (shared by dec_tile and the segment summary).  dec_prepare: the tile's
+// bytes (zero past C), the E mask (y[j] == y[j+1]: a token starting at j is 3 bytes long) and the
+// wave scan of the lanes' token-phase maps.  Positions are absolute in the stream; tokens start
+// only below Co (the end of the positions this wave owns: the stream, or its segment).
+struct DecPrep {
+    u32 w[4];
+    u32 la, left, validm, E, incl, excl;
+    DecEntry ta, tb;
+};
+__device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, u32 Co, u32 lane,
+                                               const DecEntry* tbl) {
+    DecPrep r;
+    const u32 p0 = pos + 16u * lane;
+    const u32 left = p0 < C ? C - p0 : 0u;
+    r.left = left;
+    const u32 nl = left < 16u ? left : 16u;
+    const u32 lefto = p0 < Co ? Co - p0 : 0u;
+    r.validm = lane < kOwnLanes ? lowmask(lefto < 16u ? lefto : 16u) : 0u;
+    u32* w = r.w;
+    w[0] = cur.x; w[1] = cur.y; w[2] = cur.z; w[3] = cur.w;
+    if (pos + kSlot > C) {   // last tiles: bytes at index >= C read as the stream's zero padding
+#pragma unroll
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 nb = nl > 4u * k ? (nl - 4u * k < 4u ? nl - 4u * k : 4u) : 0u;
+            w[k] &= lowmask(8u * nb);
+        }
+    }
+    const u32 la = from_next_lane(w[0] & 0xFFFFu, 0u) & 0xFFFFu;   // 2-byte lookahead
+    r.la = la;
+    const u32 NE = nz4(w[0] ^ alignbyte(w[1], w[0], 1)) | (nz4(w[1] ^ alignbyte(w[2], w[1], 1)) << 4) |
+                   (nz4(w[2] ^ alignbyte(w[3], w[2], 1)) << 8) | (nz4(w[3] ^ alignbyte(la, w[3], 1)) << 12);
+    r.E = ~NE & 0xFFFFu;
+    r.ta = tbl[r.E & 0xFFu];
+    r.tb = tbl[r.E >> 8];
+    const u32 selb = ent_sel(r.tb);
+    const u32 map = lane < kOwnLanes ? __builtin_amdgcn_perm(selb, selb, ent_sel(r.ta)) : kMapId;
+    r.incl = wave_scan_incl(map, kMapId, OpMap());
+    r.excl = from_prev_lane(r.incl, kMapId);
+    return r;
+}
+// dec_lengths: for tile-entry phase d, the token starts S, pair starts P (MP: count digit inside
+// the stream, PF: digit in the zero padding = the stream's final token), decoded length per
+// position W (bytes), the lane's decoded byte count and whether the tiled path must decline.
+// Digits '1'..'9' give d-'0'; anything else -> serial path.
+struct DecLen {
+    u32 S, PF, nout;
+    u32 W[4];
+    bool serial_lane;
+};
+__device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
+    DecLen r;
+    const u32* w = p.w;
+    const u32 dl = bfe(p.excl, 8u * d, 8);
+    const u32 mid = ent_exit(p.ta, dl);
+    const u32 S = (bfe(ent_masks(p.ta), 8u * dl, 8) | (bfe(ent_masks(p.tb), 8u * mid, 8) << 8)) & p.validm;
+    r.S = S;
+    const u32 P = S & p.E;
+    const u32 left18 = p.left < 18u ? p.left : 18u;
+    const u32 v18 = lowmask(left18);
+    const u32 MP = P & (v18 >> 2);
+    const u32 PF = P & ~(v18 >> 2);
+    r.PF = PF;
+    const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
+                       alignbyte(p.la, w[3], 2)};
+    u32 extra = 0, badb = 0;
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 mpb = nib_to_bytes(bfe(MP, 4u * k, 4));
+        const u32 dor = dg[k] | 0x80808080u;
+        const u32 lo = dor - 0x31313131u, hi = dor - 0x3A3A3A3Au;
+        const u32 dm1 = lo & 0x7F7F7F7Fu & ((mpb << 8) - mpb);   // d - '1' at pair starts
+        extra = __builtin_amdgcn_udot4(dm1, 0x01010101u, extra, false);
+        badb |= (~lo | hi | dg[k]) & (mpb << 7);
+        r.W[k] = nib_to_bytes(bfe(S, 4u * k, 4)) + dm1;        // decoded length per position
+    }
+    r.nout = bcnt(S, extra);
+    r.serial_lane = badb != 0u || (PF & (v18 >> 1)) != 0u;
+    return r;
+}
+
+__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
+                                        u32 lane, const DecEntry* tbl, uint8_t* stage, u32 trash_addr, uint8_t* dst,
+                                        u32x4 rso, DecState& st) {
+    RLE_STAMP(st.sp, 0);   // DMA wait + loop
+    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    next();   // the slot is free once read
+    const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl);
+    const DecLen ln = dec_lengths(pr, st.d);
+    const u32* w = pr.w;
+    const u32 incl = pr.incl, PF = ln.PF, nout = ln.nout;
+    const bool serial_lane = ln.serial_lane;
+    u32 W[4] = {ln.W[0], ln.W[1], ln.W[2], ln.W[3]};
+    const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, 63);
+    if (__builtin_amdgcn_ballot_w64(serial_lane) || st.out_pos + ttot > U) {
+        st.serial = 1;
+        return ~0u;
+    }
+    const uint64_t pfb = __builtin_amdgcn_ballot_w64(PF != 0u);
+    if (pfb) {   // the final token's byte extends to U
+        const u32 jf = (u32)__builtin_ctz(PF | 0x10000u) & 15u;
+        const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
+        st.tail = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+    }
+
+    RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
+    // scatter a key at each token start's decoded position; other positions write a private
+    // slot.  o2 = 2 x position; odd positions store the key from the high half (d16_hi).
+    const u32 rel0 = st.out_pos - st.flushed;
+    u32 o2 = 2u * (16u + rel0 + oincl - nout);
+    const u32 sbase = lds_addr(stage);
+    u32 xk[8];   // 0x8000 | byte, two positions per dword
+#pragma unroll
+    for (u32 m = 0; m < 8; ++m) xk[m] = __builtin_amdgcn_perm(0x80808080u, w[m >> 1], (m & 1u) ? 0x04030402u : 0x04010400u);
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) W[k] *= 2u;
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 w2 = (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+        const u32 a = w2 ? sbase + o2 + ((o2 >> 3) & ~3u) : trash_addr;
+        auto* p = reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(a);
+        if (j & 1u) *p = (uint16_t)((((o2 << 23) & 0x0F000000u) | xk[j >> 1]) >> 16);
+        else *p = (uint16_t)(((o2 << 7) & 0x0F00u) | xk[j >> 1]);
+        o2 += w2;
+    }
+    wave_lds_sync();
+    RLE_STAMP(st.sp, 2);   // scatter
+
+    const u32 newrel = rel0 + ttot;
+    const u32 nfl = newrel >> 4;
+    const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
+    if (nfl) {   // move the partial chunk to staging chunk 1
+        if (lane < 8u) {
+            u32* s32 = reinterpret_cast<u32*>(stage);
+            s32[9u + lane] = s32[9u * (nfl + 1u) + lane];
+            s32[9u * (nfl + 1u) + lane] = 0u;
+        }
+        wave_lds_sync();
+    }
+    st.flushed += 16u * nfl;
+    st.out_pos += ttot;
+    st.d = bfe(readlane(incl, 63), 8u * st.d, 8);
+    RLE_STAMP(st.sp, 7);   // partial-chunk move, state
+    return rounds;
+}
+
+// After the last tile: outputs [flushed, end) = the partial chunk still staged (decoded positions
+// < out_pos), then zeros or the final unbounded token's byte (end = U for a stream's last segment,
+// end = out_pos for the others).  Bytes below flushed + head belong to the previous segment.
+__device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane, uint8_t* stage, u32x4 rso,
+                                           uint8_t* dst) {
+    const u32 rel = st.out_pos - st.flushed;   // < 16
+    const u32 span = end - st.flushed;
+    const u32 nq = (span + 15u) >> 4;
+    const u32 tv = st.tail & 0xFFu;
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stage + 36u);
+    for (u32 q0 = 0; q0 < nq; q0 += kWave) {
+        const u32 q = q0 + lane;
+        if (q < nq) {
+            u32 ob[4] = {0u, 0u, 0u, 0u};
+            u32 cur = st.fillc;
+            for (u32 j = 0; j < 16u; ++j) {
+                u32 v = tv;
+                if (q == 0u && j < rel) {
+                    const u32 h = s16[j];
+                    cur = (h & 0x8000u) ? (h & 0xFFu) : cur;
+                    v = cur;
+                }
+                ob[j >> 2] |= v << (8u * (j & 3u));
+            }
+            const u32 j0 = q == 0u ? st.head : 0u;
+            if (16u * q + 16u <= span && j0 == 0u) {
+                u32x4 o;
+                o.x = ob[0]; o.y = ob[1]; o.z = ob[2]; o.w = ob[3];
+                vstore(rso, st.flushed + 16u * q, o);
+            } else {
+                for (u32 j = j0; j < 16u && 16u * q + j < span; ++j)
+                    dst[st.flushed + 16u * q + j] = (uint8_t)(ob[j >> 2] >> (8u * (j & 3u)));
+            }
+        }
+    }
+    wave_lds_sync();
+    if (lane < 9u) reinterpret_cast<u32*>(stage)[9u + lane] = 0u;   // staging chunk 1 back to zero
+    vm_drain();
+}
+
+// Exact serial decode (src/rleCompression.c:47-62 semantics, writes capped at cap) for the
+// streams the tiled path declines: counts outside '1'..'9', unbounded counts before the last
+// token, or streams that decode to more than U bytes.  One lane; the encoder never emits these.
+__device__ u32 dec_serial(const uint8_t* src, u32 C, u32 U, uint64_t cap, uint8_t* dst, u32 lane,
+                          uint8_t* stage) {
+    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
+        reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
+    for (uint64_t c = lane; c * 16u < cap; c += kWave) {
+        if (c * 16u + 16u <= cap) *reinterpret_cast<u32x4*>(dst + c * 16u) = u32x4{0u, 0u, 0u, 0u};
+        else
+            for (uint64_t p = c * 16u; p < cap; ++p) dst[p] = 0;
+    }
+    vm_drain();
+    wave_lds_sync();
+    u32 st = RLE_STATUS_SERIAL;
+    if (lane == 0) {
+        uint64_t o = 0, j = 0;
+        while (j < C) {
+            if (o >= cap) { st |= RLE_STATUS_OVERFLOW; break; }
+            const uint8_t v = src[j];
+            dst[o++] = v;
+            const uint8_t n1 = (j + 1 < C) ? src[j + 1] : (uint8_t)0;
+            if (v == n1) {
+                const uint8_t dgt = (j + 2 < C) ? src[j + 2] : (uint8_t)0;
+                const int occ = (int)(int8_t)dgt - 48;
+                const uint64_t ex = occ < 0 ? ~0ull : (occ >= 2 ? (uint64_t)(occ - 1) : 0ull);
+                const uint64_t room = o < U ? U - o : 0;
+                const uint64_t kk = ex < room ? ex : room;
+                for (uint64_t i = 0; i < kk; ++i) dst[o + i] = v;
+                o += kk;
+                j += 3;
+            } else {
+                j += 1;
+            }
+        }
+    }
+    vm_drain();
+    return readlane(st, 0);
+}
+
+}  // namespace rle

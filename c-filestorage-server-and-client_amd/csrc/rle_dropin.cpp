@@ -55,6 +55,10 @@ inline void check(hipError_t e, const char* what) {
 // Small-call threshold: up to this many input bytes the worst-case output is copied back in the
 // same round trip as its size (one stream sync instead of two).
 constexpr size_t kOneTripBytes = 128u << 10;
+// From these sizes one call is cut into segments processed by separate waves
+// (rle_*_batch_device_seg) instead of one wave walking the whole buffer.
+constexpr size_t kSegEncodeBytes = 48u << 10;
+constexpr size_t kSegDecodeBytes = 32u << 10;
 
 struct Ctx {
     int dev = 0;
@@ -65,6 +69,7 @@ struct Ctx {
     uint8_t* d_out = nullptr; size_t d_out_cap = 0;
     uint64_t* d_meta = nullptr;                      // [in_off, in_len, out_off, out_len, out_cap, status]
     uint64_t* h_meta = nullptr;                      // pinned mirror
+    uint8_t* d_ws = nullptr;  size_t d_ws_cap = 0;    // segmented-path workspace
 };
 
 void free_ctx(void* p) {
@@ -78,6 +83,7 @@ void free_ctx(void* p) {
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_meta);
+    (void)hipFree(c->d_ws);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -149,9 +155,13 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
     check(hipMemcpyAsync(c->d_in, c->h_in, U, hipMemcpyHostToDevice, c->s), "H2D");
     check(hipMemcpyAsync(c->d_meta, c->h_meta, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
     uint32_t* d_status = reinterpret_cast<uint32_t*>(c->d_meta + 5);
-    if (rle_encode_batch_device(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2, c->d_meta + 3,
-                                d_status, 1, c->s) != RLE_OK)
-        die("encode launch", hipGetLastError());
+    if (U >= kSegEncodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, U));
+    const int erc = U >= kSegEncodeBytes
+                        ? rle_encode_batch_device_seg(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
+                                                      c->d_meta + 3, d_status, 1, U, c->d_ws, c->d_ws_cap, c->s)
+                        : rle_encode_batch_device(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
+                                                  c->d_meta + 3, d_status, 1, c->s);
+    if (erc != RLE_OK) die("encode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_meta + 3, c->d_meta + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
     const bool one_trip = U <= kOneTripBytes;
     if (one_trip) {
@@ -207,9 +217,14 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     check(hipMemcpyAsync(c->d_in, c->h_in, C, hipMemcpyHostToDevice, c->s), "H2D");
     check(hipMemcpyAsync(c->d_meta, c->h_meta, 6 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
     uint32_t* d_status = reinterpret_cast<uint32_t*>(c->d_meta + 5);
-    if (rle_decode_batch_device(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2, c->d_meta + 3,
-                                c->d_meta + 4, d_status, 1, c->s) != RLE_OK)
-        die("decode launch", hipGetLastError());
+    if (C >= kSegDecodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, C));
+    const int drc = C >= kSegDecodeBytes
+                        ? rle_decode_batch_device_seg(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
+                                                      c->d_meta + 3, c->d_meta + 4, d_status, 1, C, c->d_ws,
+                                                      c->d_ws_cap, c->s)
+                        : rle_decode_batch_device(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
+                                                  c->d_meta + 3, c->d_meta + 4, d_status, 1, c->s);
+    if (drc != RLE_OK) die("decode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_meta + 5, c->d_meta + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
     if (U) check(hipMemcpyAsync(c->h_out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");

@@ -1,0 +1,549 @@
+// rle_segmented.hip — the codec for LARGE buffers: several waves per buffer.
+//
+// A one-wave-per-buffer launch walks a buffer's tiles one after another, so a single big buffer
+// (the drop-in's one-call-per-file path, src/filesystemApi.c:766-775, or the large end of a
+// mixed batch) runs at one wave's speed.  Here every buffer is cut into segments of 4..64 tiles
+// (1008 input bytes each; the launcher aims at ~16 segments per CU) that separate waves process.  The only state crossing a segment boundary is
+// (the algebra, checked against the oracle on CPU: tests/seg_model.py, tests/test_seg_model.py):
+//   encode  the run phase entering the segment.  A segment summary holds the offset L0 of its
+//           first run boundary, its last boundary lb, whether a boundary-free segment's run
+//           continues past it, and the compressed bytes of the tokens from L0 on; a per-buffer
+//           scan turns them into each segment's entering run start rs (a running max of lb) and
+//           output offset (the entering piece's tokens have a closed form in L0 and the phase).
+//   decode  the token phase entering the segment (0..2).  A segment summary holds, for each of
+//           the three possible entry phases, the exit phase, the decoded byte count and whether
+//           the tiled path would decline; the per-buffer scan composes the exit maps (v_perm
+//           selectors, like the in-wave scan) and sums the counts of the phases actually taken.
+// Four launches per direction: plan (segments per buffer, exclusive scan), summary (persistent
+// waves over all segments), scan (one wave per buffer), write (persistent waves over all
+// segments, the tile steps of rle_device.h with absolute positions, an owned end and a first
+// chunk shared with the previous segment written bytewise).  Same output as rle_kernels.hip.
+#include "rle_device.h"
+
+namespace rle {
+
+// Segment length: seg_tiles tiles of 1008 input bytes, a kernel argument chosen by the launcher
+// (4..64 tiles: about 16 segments per CU over the batch).
+constexpr u32 kSegTilesMin = 4, kSegTilesMax = 64;
+constexpr u32 kSegWaves = 4;
+constexpr u32 kSegBlock = kWave * kSegWaves;
+constexpr u32 kNone = 0xFFFFFFFFu;
+// per-buffer flags (workspace) written by the scans, read by the writers
+constexpr u32 kFlagSkip = 1u;     // bad buffer: status already written
+constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the whole buffer
+
+// Segments of an n-byte buffer: n = q S + r gives q + (r >= 3) segments (at least one); the last
+// absorbs a remainder of 1-2 bytes, so a stream's final token never starts a segment of its own.
+__device__ __forceinline__ u32 seg_count(u32 n, u32 sb) {
+    const u32 k = (u32)(((uint64_t)n + sb - 3u) / sb);
+    return k ? k : 1u;
+}
+__device__ __forceinline__ u32 len32(uint64_t n) { return n > kMaxBufferBytes ? 0u : (u32)n; }
+
+// seg_first[i] = segments of buffers < i; seg_first[n] = total.  One workgroup.
+__global__ __launch_bounds__(1024) void seg_plan_kernel(const uint64_t* __restrict__ len, u32 n, u32 sb,
+                                                        u32* __restrict__ seg_first) {
+    __shared__ u32 part[1024];
+    const u32 t = threadIdx.x;
+    const u32 per = (n + 1023u) / 1024u;
+    const u32 b0 = t * per < n ? t * per : n;
+    const u32 b1 = b0 + per < n ? b0 + per : n;
+    u32 s = 0;
+    for (u32 i = b0; i < b1; ++i) s += seg_count(len32(len[i]), sb);
+    part[t] = s;
+    __syncthreads();
+    for (u32 off = 1; off < 1024u; off <<= 1) {
+        const u32 v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    u32 base = t ? part[t - 1] : 0u;
+    for (u32 i = b0; i < b1; ++i) {
+        seg_first[i] = base;
+        base += seg_count(len32(len[i]), sb);
+    }
+    if (t == 1023u) seg_first[n] = part[1023];
+}
+
+// the buffer holding global segment g: seg_first[b] <= g < seg_first[b + 1] (every buffer has a
+// segment, so seg_first is strictly increasing)
+__device__ __forceinline__ u32 seg_buffer(const u32* seg_first, u32 n, u32 g) {
+    u32 lo = 0, hi = n;
+    while (hi - lo > 1u) {
+        const u32 mid = (lo + hi) >> 1;
+        if (uniform(seg_first[mid]) <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ void seg_range(u32 i, u32 nseg, u32 n, u32 sb, u32& p0, u32& p1) {
+    p0 = i * sb;
+    p1 = (i + 1u == nseg) ? n : p0 + sb;
+}
+
+__device__ __forceinline__ u32 wave_sum(u32 x) { return readlane(wave_scan_incl(x, 0u, OpAdd()), 63); }
+
+// ================================================================ ENCODE
+// compressed bytes of the tokens starting in a segment's entering run piece (length L0) when the
+// byte before the segment has run phase q; cont: the piece's run continues past the segment
+__device__ __forceinline__ u32 enc_piece_count(u32 L0, u32 q, u32 cont) {
+    const u32 k0 = q >= 8u ? 0u : 8u - q;
+    if (L0 <= k0) return 0u;
+    const u32 n = (L0 - 1u - k0) / 9u + 1u;
+    const bool last_is_start = (L0 - 1u - k0) % 9u == 0u;
+    return 3u * n - ((last_is_start && !cont) ? 2u : 0u);
+}
+
+__global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_t* __restrict__ in,
+                                                                    const uint64_t* __restrict__ in_off,
+                                                                    const uint64_t* __restrict__ in_len, u32 n,
+                                                                    const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                    uint4* __restrict__ summ) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
+        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const uint64_t U64 = in_len[b];
+        const uint8_t* src = in + in_off[b];
+        uint4 res = make_uint4(0u, 0u, 0u, 0u);
+        if (U64 > 0 && U64 <= kMaxBufferBytes && !((uintptr_t)src & 15u)) {
+            const u32 U = (u32)U64;
+            u32 p0, p1;
+            seg_range(g - s0, nseg, U, sb, p0, p1);
+            const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+            u32 prev_top = p0 ? (u32)src[p0 - 1u] << 24 : 0u;
+            u32 rs = p0, fb = kNone, lb = kNone, rest = 0;
+            walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
+                nx();
+                const EncAn an = enc_analyze(cur, p0 + t * kTileStep, U, p1, lane, prev_top, rs);
+                // run boundaries inside the segment: the first one (L0) and the last one (lb)
+                const u32 Bo = an.B & an.validm;
+                const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
+                if (bl) {
+                    const u32 fl = (u32)__builtin_ctzll(bl), ll = 63u - (u32)__builtin_clzll(bl);
+                    const u32 first = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), fl);
+                    const u32 last = readlane(an.p0 + 31u - (u32)__builtin_clz(Bo | 1u), ll);
+                    if (fb == kNone) fb = first;
+                    lb = last;
+                }
+                // tokens at or after the first boundary do not depend on the entering run phase
+                u32 fbm = 0u;
+                if (fb != kNone) fbm = fb <= an.p0 ? 0xFFFFu : (fb >= an.p0 + 16u ? 0u : ~lowmask(fb - an.p0) & 0xFFFFu);
+                rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
+                prev_top = readlane(an.top, kOwnLanes - 1u);
+                const u32 i63 = readlane(an.incl, 63);
+                rs = i63 > rs ? i63 : rs;
+                return 0u;
+            });
+            const u32 L0 = fb == kNone ? p1 - p0 : fb - p0;
+            const u32 cont = (fb == kNone && p1 < U && src[p1] == src[p1 - 1u]) ? 1u : 0u;
+            res = make_uint4(L0, lb == kNone ? 0u : lb + 1u, rest, cont);
+        }
+        if (lane == 0) summ[g] = res;
+    }
+}
+
+// one wave per buffer: entering run start and output offset of every segment, C of the buffer
+__global__ __launch_bounds__(kSegBlock) void enc_seg_scan_kernel(const uint8_t* __restrict__ in,
+                                                                 const uint64_t* __restrict__ in_off,
+                                                                 const uint64_t* __restrict__ in_len,
+                                                                 uint8_t* __restrict__ out,
+                                                                 const uint64_t* __restrict__ out_off,
+                                                                 uint64_t* __restrict__ out_len,
+                                                                 uint32_t* __restrict__ status, u32 n,
+                                                                 const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                 const uint4* __restrict__ summ, uint2* __restrict__ plan,
+                                                                 u32* __restrict__ bflag) {
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 b = blockIdx.x * kSegWaves + uniform(threadIdx.x / kWave);
+    if (b >= n) return;
+    const uint64_t U64 = in_len[b];
+    const uint8_t* src = in + in_off[b];
+    uint8_t* dst = out + out_off[b];
+    const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]);
+    u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+    if (U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
+    if (bad) {
+        if (lane == 0) {
+            out_len[b] = 0;
+            if (status) status[b] = bad;
+            bflag[b] = kFlagSkip;
+        }
+        return;
+    }
+    u32 carry_lb = 0, carry_off = 0;   // max (lb + 1) so far; output offset
+    for (u32 base = s0; base < s1; base += kWave) {
+        const u32 g = base + lane;
+        const bool valid = g < s1;
+        const uint4 sm = valid ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
+        const u32 p0 = (g - s0) * sb;
+        const u32 incl = wave_scan_incl(sm.y, 0u, OpMax());
+        const u32 ex = from_prev_lane(incl, 0u);
+        const u32 rsp1 = ex > carry_lb ? ex : carry_lb;
+        const u32 rs = rsp1 ? rsp1 - 1u : 0u;
+        const u32 piece = (valid && p0 > 0u) ? enc_piece_count(sm.x, mod9(p0 - 1u - rs), sm.w) : 0u;
+        const u32 cnt = valid ? piece + sm.z : 0u;
+        const u32 oincl = wave_scan_incl(cnt, 0u, OpAdd());
+        if (valid) plan[g] = make_uint2(rs, carry_off + oincl - cnt);
+        const u32 i63 = readlane(incl, 63);
+        carry_lb = i63 > carry_lb ? i63 : carry_lb;
+        carry_off += readlane(oincl, 63);
+    }
+    if (lane == 0) {
+        out_len[b] = carry_off;
+        if (status) status[b] = RLE_STATUS_OK;
+        bflag[b] = 0u;
+    }
+}
+
+__global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t* __restrict__ in,
+                                                                  const uint64_t* __restrict__ in_off,
+                                                                  const uint64_t* __restrict__ in_len,
+                                                                  uint8_t* __restrict__ out,
+                                                                  const uint64_t* __restrict__ out_off, u32 n,
+                                                                  const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                  const uint2* __restrict__ plan,
+                                                                  const u32* __restrict__ bflag) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kEncStage];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    uint8_t* stage = stage_all + wid * kEncStage;
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
+        const u32 b = seg_buffer(seg_first, n, g);
+        if (uniform(bflag[b])) continue;
+        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const u32 U = (u32)in_len[b];
+        const uint8_t* src = in + in_off[b];
+        uint8_t* dst = out + out_off[b];
+        u32 p0, p1;
+        seg_range(g - s0, nseg, U, sb, p0, p1);
+        const uint2 pl = plan[g];
+        const u32 rs = uniform(pl.x), off = uniform(pl.y);
+        const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+        const u32x4 rso = make_rsrc(dst, U + U / 2u);
+        EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, {}};
+        walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+            return enc_tile(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st);
+        });
+        // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past this
+        // segment's output and nothing before it
+        if (lane >= st.head && lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
+        wave_lds_sync();
+    }
+}
+
+// ================================================================ DECODE
+__global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_t* __restrict__ in,
+                                                                    const uint64_t* __restrict__ in_off,
+                                                                    const uint64_t* __restrict__ in_len, u32 n,
+                                                                    const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                    uint4* __restrict__ summ) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
+    __shared__ DecEntry tbl[256];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    for (u32 k = threadIdx.x; k < 256u; k += kSegBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
+    __syncthreads();
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
+        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const uint64_t C64 = in_len[b];
+        const uint8_t* src = in + in_off[b];
+        uint4 res = make_uint4(0u, 0u, 0u, 0u | (1u << 2) | (2u << 4));   // empty: counts 0, exit = entry
+        if (C64 > 0 && C64 <= kMaxBufferBytes && !((uintptr_t)src & 15u)) {
+            const u32 C = (u32)C64;
+            u32 q0, q1;
+            seg_range(g - s0, nseg, C, sb, q0, q1);
+            const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+            u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
+            walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
+                nx();
+                const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl);
+                const u32 m63 = readlane(pr.incl, 63);
+                if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
+                    const DecLen ln = dec_lengths(pr, d0);
+                    const u32 tot = wave_sum(ln.nout);
+                    const bool bad = __builtin_amdgcn_ballot_w64(ln.serial_lane) != 0;
+                    c0 += tot; c1 += tot; c2 += tot;
+                    badm |= bad ? 7u : 0u;
+                    d0 = d1 = d2 = bfe(m63, 8u * d0, 8);
+                } else {
+                    const DecLen l0 = dec_lengths(pr, d0);
+                    c0 += wave_sum(l0.nout);
+                    badm |= __builtin_amdgcn_ballot_w64(l0.serial_lane) ? 1u : 0u;
+                    const DecLen l1 = dec_lengths(pr, d1);
+                    c1 += wave_sum(l1.nout);
+                    badm |= __builtin_amdgcn_ballot_w64(l1.serial_lane) ? 2u : 0u;
+                    const DecLen l2 = dec_lengths(pr, d2);
+                    c2 += wave_sum(l2.nout);
+                    badm |= __builtin_amdgcn_ballot_w64(l2.serial_lane) ? 4u : 0u;
+                    d0 = bfe(m63, 8u * d0, 8);
+                    d1 = bfe(m63, 8u * d1, 8);
+                    d2 = bfe(m63, 8u * d2, 8);
+                }
+                return 0u;
+            });
+            res = make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8));
+        }
+        if (lane == 0) summ[g] = res;
+    }
+}
+
+// one wave per buffer: entry phase and output offset of every segment; serial when the taken
+// path declines anywhere or decodes past U
+__global__ __launch_bounds__(kSegBlock) void dec_seg_scan_kernel(const uint8_t* __restrict__ in,
+                                                                 const uint64_t* __restrict__ in_off,
+                                                                 const uint64_t* __restrict__ in_len,
+                                                                 uint8_t* __restrict__ out,
+                                                                 const uint64_t* __restrict__ out_off,
+                                                                 const uint64_t* __restrict__ out_len,
+                                                                 const uint64_t* __restrict__ out_cap,
+                                                                 uint32_t* __restrict__ status, u32 n,
+                                                                 const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                 const uint4* __restrict__ summ, uint2* __restrict__ plan,
+                                                                 u32* __restrict__ bflag) {
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 b = blockIdx.x * kSegWaves + uniform(threadIdx.x / kWave);
+    if (b >= n) return;
+    const uint64_t C64 = in_len[b], U64 = out_len[b];
+    const uint64_t cap = out_cap ? out_cap[b] : U64;
+    const uint8_t* src = in + in_off[b];
+    uint8_t* dst = out + out_off[b];
+    const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]);
+    u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
+    if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
+    if (bad) {
+        if (lane == 0) {
+            if (status) status[b] = bad;
+            bflag[b] = kFlagSkip;
+        }
+        return;
+    }
+    const u32 U = (u32)U64;
+    u32 e_carry = 0, carry_off = 0;
+    bool serial = false;
+    for (u32 base = s0; base < s1; base += kWave) {
+        const u32 g = base + lane;
+        const bool valid = g < s1;
+        const uint4 sm = valid ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
+        const u32 sel = valid ? (bfe(sm.w, 0, 2) | (bfe(sm.w, 2, 2) << 8) | (bfe(sm.w, 4, 2) << 16) | (3u << 24)) : kMapId;
+        const u32 incl = wave_scan_incl(sel, kMapId, OpMap());
+        const u32 e = bfe(from_prev_lane(incl, kMapId), 8u * e_carry, 8);
+        const u32 cnt = valid ? (e == 0u ? sm.x : (e == 1u ? sm.y : sm.z)) : 0u;
+        serial |= __builtin_amdgcn_ballot_w64(valid && ((sm.w >> (8u + e)) & 1u)) != 0;
+        const u32 oincl = wave_scan_incl(cnt, 0u, OpAdd());
+        if (valid) plan[g] = make_uint2(e, carry_off + oincl - cnt);
+        e_carry = bfe(readlane(incl, 63), 8u * e_carry, 8);
+        const u32 add = readlane(oincl, 63);
+        if (add > U - (carry_off < U ? carry_off : U)) serial = true;   // decodes past U
+        carry_off += add;
+    }
+    if (lane == 0) bflag[b] = serial ? kFlagSerial : 0u;
+}
+
+__global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t* __restrict__ in,
+                                                                  const uint64_t* __restrict__ in_off,
+                                                                  const uint64_t* __restrict__ in_len,
+                                                                  uint8_t* __restrict__ out,
+                                                                  const uint64_t* __restrict__ out_off,
+                                                                  const uint64_t* __restrict__ out_len,
+                                                                  const uint64_t* __restrict__ out_cap,
+                                                                  uint32_t* __restrict__ status, u32 n,
+                                                                  const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                  const uint2* __restrict__ plan,
+                                                                  const u32* __restrict__ bflag) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kDecStage];
+    __shared__ __attribute__((aligned(16))) uint16_t trash_all[kSegWaves * kWave];
+    __shared__ DecEntry tbl[256];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    for (u32 k = threadIdx.x; k < 256u; k += kSegBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
+    uint8_t* stage = stage_all + wid * kDecStage;
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    const u32 trash_addr = lds_addr(trash_all + wid * kWave + lane);
+    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
+        reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
+        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 flag = uniform(bflag[b]);
+        if (flag & kFlagSkip) continue;
+        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const u32 C = (u32)in_len[b], U = (u32)out_len[b];
+        const uint8_t* src = in + in_off[b];
+        uint8_t* dst = out + out_off[b];
+        if (flag & kFlagSerial) {   // one wave decodes the whole buffer exactly
+            if (g == s0) {
+                const uint64_t cap = out_cap ? out_cap[b] : (uint64_t)U;
+                const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage);
+                if (lane == 0 && status) status[b] = stat;
+            }
+            continue;
+        }
+        u32 q0, q1;
+        seg_range(g - s0, nseg, C, sb, q0, q1);
+        const uint2 pl = plan[g];
+        const u32 e = uniform(pl.x), off = uniform(pl.y);
+        const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+        const u32x4 rso = make_rsrc(dst, U);
+        DecState st{off, off & ~15u, e, 0u, 0u, 0u, off & 15u, {}};
+        walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+            return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, trash_addr, dst, rso, st);
+        });
+        const bool last = g + 1u == s0 + nseg;
+        dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
+        if (last && lane == 0 && status) status[b] = st.serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : RLE_STATUS_OK;
+    }
+}
+
+}  // namespace rle
+
+// ================================================================ C-ABI launchers
+#include <map>
+#include <mutex>
+#include <utility>
+
+namespace {
+// The workspace (seg_first, per-segment summaries and plans, per-buffer flags) belongs to the
+// caller (rle_seg_workspace_bytes), like a cub temp-storage argument: the library keeps no
+// device memory between calls and nothing tied to a stream or thread.  Host-side cache: CUs.
+struct CuCache {
+    std::mutex m;
+    std::map<int, int> cus;
+};
+CuCache& cu_cache() {
+    static CuCache* p = new CuCache();   // never destroyed: launches may run during exit
+    return *p;
+}
+// 256 B-aligned carve-up of the workspace
+struct Carve {
+    uint32_t* seg_first;
+    uint4* summ;
+    uint2* plan;
+    uint32_t* bflag;
+    size_t bytes;
+};
+inline size_t al(size_t x) { return (x + 255u) & ~(size_t)255u; }
+Carve carve(char* base, uint32_t n, uint32_t maxseg) {
+    Carve c;
+    size_t o = 0;
+    c.seg_first = reinterpret_cast<uint32_t*>(base + o); o += al(sizeof(uint32_t) * ((size_t)n + 1));
+    c.summ = reinterpret_cast<uint4*>(base + o);         o += al(sizeof(uint4) * (size_t)maxseg);
+    c.plan = reinterpret_cast<uint2*>(base + o);         o += al(sizeof(uint2) * (size_t)maxseg);
+    c.bflag = reinterpret_cast<uint32_t*>(base + o);     o += al(sizeof(uint32_t) * (size_t)n);
+    c.bytes = o;
+    return c;
+}
+// upper bound on the segments of n buffers holding total bytes (each segment but a buffer's
+// last covers sb bytes)
+inline uint32_t max_segments(uint32_t n, uint64_t total, uint32_t sb) {
+    const uint64_t m = total / (sb - 2u) + n;
+    return m > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)m;
+}
+int device_cus(int* ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return RLE_E_HIP;
+    CuCache& P = cu_cache();
+    std::lock_guard<std::mutex> g(P.m);
+    auto c = P.cus.find(dev);
+    if (c == P.cus.end()) {
+        int k = 0;
+        if (hipDeviceGetAttribute(&k, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || k <= 0) k = 256;
+        c = P.cus.emplace(dev, k).first;
+    }
+    *ncu = c->second;
+    return RLE_OK;
+}
+// segment length in bytes: about 16 segments per CU over the batch, 4..64 tiles each
+inline uint32_t seg_bytes(uint64_t total, int ncu) {
+    const uint64_t tiles = (total + rle::kTileStep - 1) / rle::kTileStep;
+    uint64_t per = tiles / ((uint64_t)ncu * 16u);
+    per = per < rle::kSegTilesMin ? rle::kSegTilesMin : (per > rle::kSegTilesMax ? rle::kSegTilesMax : per);
+    return (uint32_t)per * rle::kTileStep;
+}
+// persistent grids: enough workgroups to fill every CU (4 per CU), never more than the segments
+inline uint32_t seg_grid(uint32_t maxseg, int ncu) {
+    const uint32_t need = (maxseg + rle::kSegWaves - 1) / rle::kSegWaves;
+    const uint32_t fill = (uint32_t)ncu * 4u;
+    const uint32_t g = need < fill ? need : fill;
+    return g ? g : 1u;
+}
+inline uint32_t buf_grid(uint32_t n) { return (n + rle::kSegWaves - 1) / rle::kSegWaves; }
+}  // namespace
+
+extern "C" size_t rle_seg_workspace_bytes(uint32_t n, uint64_t total_in_bytes) {
+    int ncu = 0;
+    if (device_cus(&ncu) != RLE_OK) ncu = 256;
+    const uint32_t sb = seg_bytes(total_in_bytes, ncu);
+    return carve(nullptr, n, max_segments(n, total_in_bytes, sb)).bytes;
+}
+
+extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                           void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                                           uint32_t* d_status, uint32_t n, uint64_t total_in_bytes, void* d_workspace,
+                                           size_t workspace_bytes, void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    int ncu = 0;
+    if (const int rc = device_cus(&ncu)) return rc;
+    const uint32_t sb = seg_bytes(total_in_bytes, ncu);
+    const uint32_t maxseg = max_segments(n, total_in_bytes, sb);
+    const Carve w = carve(static_cast<char*>(d_workspace), n, maxseg);
+    if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
+    const uint8_t* in = (const uint8_t*)d_in;
+    uint8_t* out = (uint8_t*)d_out;
+    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first);
+    hipLaunchKernelGGL(rle::enc_seg_summary_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                       d_in_off, d_in_len, n, w.seg_first, maxseg, sb, w.summ);
+    hipLaunchKernelGGL(rle::enc_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
+                       out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
+    hipLaunchKernelGGL(rle::enc_seg_write_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                       d_in_off, d_in_len, out, d_out_off, n, w.seg_first, maxseg, sb, w.plan, w.bflag);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
+
+extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                           void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                                           const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
+                                           uint64_t total_in_bytes, void* d_workspace, size_t workspace_bytes,
+                                           void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    int ncu = 0;
+    if (const int rc = device_cus(&ncu)) return rc;
+    const uint32_t sb = seg_bytes(total_in_bytes, ncu);
+    const uint32_t maxseg = max_segments(n, total_in_bytes, sb);
+    const Carve w = carve(static_cast<char*>(d_workspace), n, maxseg);
+    if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
+    const uint8_t* in = (const uint8_t*)d_in;
+    uint8_t* out = (uint8_t*)d_out;
+    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first);
+    hipLaunchKernelGGL(rle::dec_seg_summary_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                       d_in_off, d_in_len, n, w.seg_first, maxseg, sb, w.summ);
+    hipLaunchKernelGGL(rle::dec_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
+                       out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
+    hipLaunchKernelGGL(rle::dec_seg_write_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                       d_in_off, d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, maxseg, sb,
+                       w.plan, w.bflag);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}

@@ -58,6 +58,12 @@ def lib():
     L.rle_encode_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, vp]
     L.rle_decode_batch_device.restype = ctypes.c_int
     L.rle_decode_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.rle_seg_workspace_bytes.restype = sz
+    L.rle_seg_workspace_bytes.argtypes = [u32, ctypes.c_uint64]
+    L.rle_encode_batch_device_seg.restype = ctypes.c_int
+    L.rle_encode_batch_device_seg.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, ctypes.c_uint64, vp, sz, vp]
+    L.rle_decode_batch_device_seg.restype = ctypes.c_int
+    L.rle_decode_batch_device_seg.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, ctypes.c_uint64, vp, sz, vp]
     L.rle_gen_synthetic_device.restype = ctypes.c_int
     L.rle_gen_synthetic_device.argtypes = [vp, vp, vp, vp, vp, u32, vp]
     L.rle_mi355x_selftest.restype = ctypes.c_int
@@ -148,6 +154,46 @@ def decode_batch(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, st
                                        _ptr(out_len), _ptr(out_cap), _ptr(status), n, _stream_ptr(stream))
     if rc != RLE_OK:
         raise RLEError(f"rle_decode_batch_device failed: {rc}")
+
+
+def seg_workspace(n: int, total_in_bytes: int, device=None):
+    """A device workspace for the segmented entry points (caller-owned, reusable across calls on
+    one stream)."""
+    import torch
+    nb = int(lib().rle_seg_workspace_bytes(n, int(total_in_bytes)))
+    return torch.empty(nb + 256, dtype=torch.uint8, device=device if device is not None else "cuda")
+
+
+def _ws_ptr(ws):
+    a = ws.data_ptr()
+    return ctypes.c_void_p((a + 255) & ~255), ws.numel() - ((-a) & 255)
+
+
+def encode_batch_seg(d_in, in_off, in_len, d_out, out_off, out_len, status=None, total_in_bytes=None,
+                     workspace=None, stream=None):
+    """Segmented batched encode (several waves per buffer; for large buffers)."""
+    n = in_off.numel()
+    total = int(in_len.sum().item()) if total_in_bytes is None else int(total_in_bytes)
+    ws = workspace if workspace is not None else seg_workspace(n, total, d_in.device)
+    wp, wn = _ws_ptr(ws)
+    rc = lib().rle_encode_batch_device_seg(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                           _ptr(out_len), _ptr(status), n, total, wp, wn, _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_encode_batch_device_seg failed: {rc}")
+
+
+def decode_batch_seg(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, status=None,
+                     total_in_bytes=None, workspace=None, stream=None):
+    """Segmented batched decode (several waves per buffer; for large buffers)."""
+    n = in_off.numel()
+    total = int(in_len.sum().item()) if total_in_bytes is None else int(total_in_bytes)
+    ws = workspace if workspace is not None else seg_workspace(n, total, d_in.device)
+    wp, wn = _ws_ptr(ws)
+    rc = lib().rle_decode_batch_device_seg(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                           _ptr(out_len), _ptr(out_cap), _ptr(status), n, total, wp, wn,
+                                           _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_decode_batch_device_seg failed: {rc}")
 
 
 def gen_synthetic(d_out, off, length, kind=None, index=None, stream=None):

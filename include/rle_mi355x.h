@@ -81,6 +81,29 @@ int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
 /* Runs the cross-lane (DPP) primitive self-test on the current device; 0 = pass. */
 int rle_mi355x_selftest(void);
 
+/* Large buffers: the same batched encode / decode with every buffer cut into segments of 4..64
+ * tiles of 1008 input bytes (about 16 segments per CU over the batch) processed by separate waves
+ * (per-segment summaries, a per-buffer scan of the run / token phase crossing segment boundaries,
+ * then per-segment writes: four launches).  Same arguments, results and status codes as
+ * rle_encode_batch_device / rle_decode_batch_device, plus:
+ *   total_in_bytes  >= the sum of the n input lengths (sizes the segment tables; a buffer whose
+ *                   segments do not fit gets RLE_STATUS_TOOLARGE)
+ *   d_workspace     caller-owned device memory of at least rle_seg_workspace_bytes(n,
+ *                   total_in_bytes) bytes, 256-byte aligned, not used by another launch in flight
+ * Use it when buffers are large relative to the batch (one big file, a mixed 4 KiB - 1 MiB batch);
+ * RLEcompress / RLEdecompress use it from 48 KiB (encode input) / 32 KiB (decode input).
+ * Replaces src/rleCompression.c:9-62 like the entries above. */
+size_t rle_seg_workspace_bytes(uint32_t n, uint64_t total_in_bytes);
+int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                                uint32_t* d_status, uint32_t n, uint64_t total_in_bytes,
+                                void* d_workspace, size_t workspace_bytes, void* stream);
+int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                                const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
+                                uint64_t total_in_bytes, void* d_workspace, size_t workspace_bytes,
+                                void* stream);
+
 /* Diagnostic builds only (RLE_STAMPS=1, never the product library): per-segment decode cycle sums
  * over all waves: [tile wait, scan, scatter, flush reads, flush fill, flush store, flush re-zero,
  * move/drain/finish, waves]; RLE_E_INVAL otherwise. */

@@ -26,8 +26,9 @@ def _i64(vals):
     return torch.tensor(np.asarray(vals, dtype=np.int64), device=DEV)
 
 
-def gpu_encode(bufs):
-    """Encode a list of byte strings in ONE batched launch; returns (outputs, status)."""
+def gpu_encode(bufs, seg=False):
+    """Encode a list of byte strings in ONE batched launch (seg: the segmented multi-wave form);
+    returns (outputs, status)."""
     n = len(bufs)
     sizes = [len(b) for b in bufs]
     in_offs, in_total = R.layout(sizes)
@@ -39,7 +40,8 @@ def gpu_encode(bufs):
     d_out = torch.full((out_total + 16,), POISON, dtype=torch.uint8, device=DEV)
     out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
-    R.encode_batch(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status)
+    (R.encode_batch_seg if seg else R.encode_batch)(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs),
+                                                    out_len, status)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
     lens = out_len.cpu().numpy()
@@ -52,7 +54,7 @@ def gpu_encode(bufs):
     return res, status.cpu().numpy()
 
 
-def gpu_decode(streams, usizes, caps=None, poison=True):
+def gpu_decode(streams, usizes, caps=None, poison=True, seg=False):
     n = len(streams)
     caps = caps if caps is not None else list(usizes)
     in_offs, in_total = R.layout([len(s) for s in streams])
@@ -63,8 +65,8 @@ def gpu_decode(streams, usizes, caps=None, poison=True):
     d_in = torch.from_numpy(host).to(DEV)
     d_out = torch.full((out_total + 16,), POISON if poison else 0, dtype=torch.uint8, device=DEV)
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
-    R.decode_batch(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out, _i64(out_offs), _i64(usizes),
-                   _i64(caps), status)
+    (R.decode_batch_seg if seg else R.decode_batch)(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out,
+                                                    _i64(out_offs), _i64(usizes), _i64(caps), status)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
     res = [out[o:o + c].tobytes() for o, c in zip(out_offs, caps)]

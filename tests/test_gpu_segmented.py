@@ -1,0 +1,90 @@
+"""GPU parity of the SEGMENTED codec (several waves per buffer: rle_*_batch_device_seg, the path the
+drop-in takes for large files) against the oracle, bit-exact.  Segments are 64512 input bytes;
+the cases sit on and around segment edges, carry runs and token phases across them (including
+'9' runs, whose decode phases never re-synchronise), mix buffer sizes, and feed invalid streams
+that must fall back to the exact serial decoder.  The algebra itself is pinned on CPU by
+tests/test_seg_model.py."""
+import numpy as np
+import pytest
+
+import rle_mi355x as R
+import rle_oracle as O
+from test_gpu_parity import gpu_decode, gpu_encode
+
+pytestmark = pytest.mark.gpu
+S = 64512
+
+
+def _parity(xs):
+    ys, st = gpu_encode(xs, seg=True)
+    assert (st == 0).all(), st
+    for i, x in enumerate(xs):
+        ref = O.encode(x)
+        assert ys[i] == ref, (i, len(x), len(ys[i]), len(ref))
+    dec, st = gpu_decode(ys, [len(x) for x in xs], seg=True)
+    for i, x in enumerate(xs):
+        assert dec[i] == x, (i, len(x))
+    assert ((st & 0xFF) == 0).all(), st
+    return ys
+
+
+def test_segment_edge_sizes():
+    xs = []
+    for k in (1, 2, 3):
+        for d in (-3, -2, -1, 0, 1, 2, 3, 4, 17):
+            for kind in range(5):
+                xs.append(O.gen(kind, 100 * k + d + 7, k * S + d))
+    xs += [b"", b"a", bytes(5), O.gen(1, 1, 1000)]
+    _parity(xs)
+
+
+def test_runs_and_phases_across_segments():
+    xs = [bytes(3 * S + 5), b"\xff" * (2 * S + 2), b"9" * (2 * S + 7), b"3" * (S + 3), b"99" * S]
+    for k in (1, 2, 5, 8, 9, 10, 17, 100):   # a run ending / starting k bytes around a segment edge
+        xs.append(b"a" * (S - k) + b"b" * (2 * k + 9) + b"c" * 1000)
+        xs.append(O.gen(1, k, S - k) + b"z" * (k + 40) + O.gen(3, k, S))
+    # compressed streams whose segment edges fall inside 3-byte tokens at every offset
+    for k in range(6):
+        xs.append(b"x" * k + b"aaab" * (S // 4 + 10))
+    _parity(xs)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_large_buffers_per_kind(kind):
+    xs = [O.gen(kind, 7, 4 << 20), O.gen(kind, 8, (1 << 20) + 12345)]
+    _parity(xs)
+
+
+def test_mixed_batch_same_as_one_wave_path():
+    rng = np.random.default_rng(11)
+    xs = []
+    for i in range(96):
+        U = int(2 ** rng.uniform(12, 20)) + int(rng.integers(0, 64))
+        xs.append(O.gen(i % 4, i, U))
+    ys_seg = _parity(xs)
+    ys_one, st = gpu_encode(xs)
+    assert ys_one == ys_seg and (st == 0).all()
+
+
+def test_invalid_streams_take_the_serial_path():
+    good = O.encode(O.gen(2, 3, 3 * S))
+    bad_digit = bytearray(good)
+    pos = 2 * S + 100
+    while not (bad_digit[pos] == bad_digit[pos + 1]):
+        pos += 1
+    bad_digit[pos + 2] = ord(":")            # count digit outside '1'..'9'
+    streams = [bytes(bad_digit), good, good[:-1] + b"q", b"aa9" * 40000, b"\x07" * (S + 10) + b"\x00"]
+    us = [3 * S, 3 * S, 3 * S, 10 * S, 2 * S]
+    caps = [u + 64 for u in us]
+    dec, st = gpu_decode(streams, us, caps, poison=False, seg=True)
+    for i, (y, U, cap) in enumerate(zip(streams, us, caps)):
+        ref, _ = O.decode(y, U, cap)
+        assert dec[i] == ref, i
+    assert st[0] & R.RLE_STATUS_SERIAL
+
+
+def test_dropin_large_files_roundtrip():
+    for x in (O.gen(1, 5, 3 << 20), bytes(2 << 20), O.gen(3, 6, (1 << 20) + 1)):
+        y = R.compress(x)
+        assert y == O.encode(x)
+        assert R.decompress(y, len(x), 5) == x + bytes(5)

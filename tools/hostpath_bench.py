@@ -86,21 +86,26 @@ def threads(T, U, seconds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=1.0)
+    ap.add_argument("--only", choices=["single", "threads"], default=None)
     a = ap.parse_args()
     R.dropin_stats(reset=True)
     res = {"single": [], "threads": []}
-    for U in (4096, 65536, 1 << 20, 4 << 20):
-        for kind in ("random", "zero", "runs"):
-            res["single"].append(one(kind, U, a.seconds))
-    for T in (1, 4, 8):
-        res["threads"].append(threads(T, 1 << 20, a.seconds))
+    if a.only != "threads":
+        for U in (4096, 65536, 1 << 20, 4 << 20):
+            for kind in ("random", "zero", "runs"):
+                res["single"].append(one(kind, U, a.seconds))
+    if a.only != "single":
+        for T in (1, 4, 8):
+            res["threads"].append(threads(T, 1 << 20, a.seconds))
+            print(f"threads {T} done", file=sys.stderr, flush=True)
     s = R.dropin_stats()
     res["dropin_stats"] = s
     tot = s["ns_stage_in"] + s["ns_device"] + s["ns_stage_out"]
     res["phase_share"] = {k: s[k] / tot for k in ("ns_stage_in", "ns_device", "ns_stage_out")} if tot else None
     res["pcie_GBps_device_phase"] = (s["bytes_h2d"] + s["bytes_d2h"]) / (s["ns_device"] * 1e-9) / 1e9 \
         if s["ns_device"] else None
-    print(json.dumps(res))
+    print(json.dumps(res), flush=True)
+    print("main done", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

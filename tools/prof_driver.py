@@ -15,9 +15,11 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="dec64k")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--seg", action="store_true", help="segmented (several waves per buffer) entry points")
 a = ap.parse_args()
 torch.cuda.set_device(0)
 B = bench.Batch(bench.WORKLOADS[a.workload], 0, 1, torch.device("cuda", 0))
+B.seg = a.seg
 s = torch.cuda.current_stream()
 B.encode(s)
 torch.cuda.synchronize()
