@@ -6,7 +6,7 @@ TAG=${1:-iter}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 600 python -m pytest $R/tests -m gpu -x -q > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/status
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python $R/bench.py --no-cpu > $O/bench.json 2> $O/bench.err
