@@ -84,8 +84,9 @@ class Batch:
         kinds = wl["kinds"]
         gidx = [k * world + rank for k in range(n)]   # shard.shard_indices(n * world, rank, world)
         sizes = [wl["size"] if wl["size"] else mixed_size(i) for i in gidx]
-        offs, total = R.layout(sizes)
-        coffs, ctotal = R.compressed_slots(sizes)
+        pad = int(os.environ.get("RLE_BENCH_PAD", "0"))   # layout experiments: spare bytes per buffer
+        offs, total = R.layout(sizes, pad=pad)
+        coffs, ctotal = R.compressed_slots(sizes, pad=pad)
         self.c_cap = ctotal
         self.ws_enc = R.seg_workspace(n, sum(sizes), dev)
         self.ws_dec = R.seg_workspace(n, ctotal, dev)

@@ -447,13 +447,20 @@ __device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e.y, 8u 
 __device__ __forceinline__ u32 ent_sel(DecEntry e) { return e.y; }
 #endif
 
-// Staging (per wave): decoded position r (biased by 16: chunk 0 is never stored) holds a u16:
-// 0 = no token starts here, else 0x8000 | (r & 15) << 8 | byte at a token start.  Within a
-// 16-aligned chunk the keys grow with position (and survive moving the chunk), so a packed-u16
-// prefix max fills each run from its start.  Chunks sit at a 36-byte stride (16 x 2 B + 4 B pad) against bank conflicts.
+// Staging (per wave): decoded position r (biased by 16: chunk 0 is a guard, never stored) holds a
+// u16 key: 0 = empty, else (r & 31) << 11 | 0x100 | byte.  Chunk c is the 32 bytes at 32 c (no
+// padding: the flush reads and re-zeroes a chunk with two 16-byte accesses).  Within a 16-aligned
+// chunk the keys grow with position, so a packed-u16 prefix max fills each run from its key.
+// Every token start writes its key at its decoded position.  Every other valid position (the
+// second byte and the count digit of a 3-byte token) writes the key of the byte before it (which
+// is its token's byte) at the position before the running offset (its token's last decoded
+// position): a correct, redundant key, so no position needs a trash slot or a select.  Positions
+// past the owned range write at the running offset, past the tile's output; the next tile's first
+// key overwrites that slot.  A token decodes to at most 9 bytes, so every 16-byte chunk holds a
+// key, and the byte entering a chunk is the last key of the chunk before it.
 constexpr u32 kDecChunks = 192;              // >= ceil((16 + 15 + 3024 + 1) / 16)
-constexpr u32 kDecStage = 36u * kDecChunks;  // bytes per wave
-__device__ __forceinline__ u32 dpad(u32 r) { return 2u * r + ((r >> 4) << 2); }
+constexpr u32 kDecStage = 32u * kDecChunks;  // bytes per wave (a multiple of 64: tags = position & 31)
+constexpr u32 kKeyFlag = 0x100u;
 
 struct DecState {
     u32 out_pos;   // decoded bytes produced so far
@@ -463,8 +470,24 @@ struct DecState {
     u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
     u32 serial;    // 1 -> stream needs the exact serial path
     u32 head;      // leading bytes of the first stored chunk that belong to the previous segment
+    u32 prev;      // stream byte before the current tile, in bits 24..31
     Stamps sp;     // diagnostic builds only
 };
+
+// v + byte k of x (one SDWA add)
+template <int kByte>
+__device__ __forceinline__ u32 add_byte(u32 v, u32 x) {
+    u32 r;
+    if constexpr (kByte == 0)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(v), "v"(x));
+    else if constexpr (kByte == 1)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(v), "v"(x));
+    else if constexpr (kByte == 2)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(v), "v"(x));
+    else
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(v), "v"(x));
+    return r;
+}
 
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
@@ -473,30 +496,28 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
         const bool active = c < nfl;
-        u32* s32 = reinterpret_cast<u32*>(stage + 36u * (c + 1u));
-        u32 L[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        u32x4* s4 = reinterpret_cast<u32x4*>(stage + 32u * (c + 1u));
+        u32x4 a = u32x4{0u, 0u, 0u, 0u}, b = a;
         if (active) {
-#pragma unroll
-            for (u32 m = 0; m < 8; ++m) L[m] = s32[m];
+            a = s4[0];
+            b = s4[1];
         }
         RLE_STAMP(sp, 3);   // flush: staging reads
+        u32 L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         // prefix max of the keys inside the chunk: within each pair, then across pairs
 #pragma unroll
         for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
 #pragma unroll
         for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m - 1], L[m - 1], 0x03020302u));
-        const u32 lastk = L[7] >> 16;
-        const u32 lv = (lastk & 0x8000u) ? (0x100u | (lastk & 0xFFu)) : 0u;
-        const u32 incl = wave_scan_incl(lv, 0u, OpLatest());
-        const u32 before = from_prev_lane(incl, 0u);
-        const u32 carry = (before ? before : fillc) & 0xFFu;
+        const u32 lastb = bfe(L[7], 16, 8);   // byte of the chunk's last key = its last output byte
+        const u32 carry = from_prev_lane(lastb, fillc);
         const u32 crep = carry * 0x00010001u;
         u32x4 o;
         o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
         o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
         o.z = __builtin_amdgcn_perm(pkmax(L[5], crep), pkmax(L[4], crep), 0x06040200u);
         o.w = __builtin_amdgcn_perm(pkmax(L[7], crep), pkmax(L[6], crep), 0x06040200u);
-        RLE_STAMP(sp, 4);   // flush: fill + carry scan
+        RLE_STAMP(sp, 4);   // flush: fill + carry
         const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
         vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o);   // RLE_NOSTORE: diagnostic
         if (skip && active) {
@@ -506,11 +527,11 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         head = 0;
         RLE_STAMP(sp, 5);   // flush: store issue
         if (active) {
-#pragma unroll
-            for (u32 m = 0; m < 8; ++m) s32[m] = 0u;
+            s4[0] = u32x4{0u, 0u, 0u, 0u};
+            s4[1] = u32x4{0u, 0u, 0u, 0u};
         }
         const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
-        fillc = readlane(o.w >> 24, lastlane);
+        fillc = readlane(lastb, lastlane);
         wave_lds_sync();
         RLE_STAMP(sp, 6);   // flush: re-zero + sync
     }
@@ -597,9 +618,25 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     return r;
 }
 
+// Scatter one dword's four positions: position 4k+i writes key(t) at staging byte address t =
+// base + byte i of X (X: the exclusive byte prefix of the doubled lengths, +2 for starts and
+// past-range positions, +0 for token-interior positions).
+template <int kHalf>
+__device__ __forceinline__ void dec_put(u32 t, u32 xk) {
+    auto* p = reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(t);
+    if constexpr (kHalf == 0) *p = (uint16_t)((t << 10) | xk);
+    else *p = (uint16_t)(((t << 26) | xk) >> 16);
+}
+__device__ __forceinline__ void dec_scatter4(u32 base, u32 X, u32 xk_lo, u32 xk_hi) {
+    dec_put<0>(add_byte<0>(base, X), xk_lo);
+    dec_put<1>(add_byte<1>(base, X), xk_lo);
+    dec_put<0>(add_byte<2>(base, X), xk_hi);
+    dec_put<1>(add_byte<3>(base, X), xk_hi);
+}
+
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
-                                        u32 lane, const DecEntry* tbl, uint8_t* stage, u32 trash_addr, uint8_t* dst,
-                                        u32x4 rso, DecState& st) {
+                                        u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
+                                        DecState& st) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
@@ -608,7 +645,6 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32* w = pr.w;
     const u32 incl = pr.incl, PF = ln.PF, nout = ln.nout;
     const bool serial_lane = ln.serial_lane;
-    u32 W[4] = {ln.W[0], ln.W[1], ln.W[2], ln.W[3]};
     const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
     const u32 ttot = readlane(oincl, 63);
     if (__builtin_amdgcn_ballot_w64(serial_lane) || st.out_pos + ttot > U) {
@@ -623,24 +659,25 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     }
 
     RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
-    // scatter a key at each token start's decoded position; other positions write a private
-    // slot.  o2 = 2 x position; odd positions store the key from the high half (d16_hi).
+    // key values: a start's own byte, an interior position's previous byte (its token's byte)
+    const u32 NS = pr.validm & ~ln.S;
+    const u32 ptop = from_prev_lane(w[3], st.prev);
+    const u32 prevw[4] = {alignbyte(w[0], ptop, 3), alignbyte(w[1], w[0], 3), alignbyte(w[2], w[1], 3),
+                          alignbyte(w[3], w[2], 3)};
     const u32 rel0 = st.out_pos - st.flushed;
-    u32 o2 = 2u * (16u + rel0 + oincl - nout);
-    const u32 sbase = lds_addr(stage);
-    u32 xk[8];   // 0x8000 | byte, two positions per dword
+    u32 base = lds_addr(stage) + 2u * (16u + rel0 + oincl - nout) - 2u;
 #pragma unroll
-    for (u32 m = 0; m < 8; ++m) xk[m] = __builtin_amdgcn_perm(0x80808080u, w[m >> 1], (m & 1u) ? 0x04030402u : 0x04010400u);
-#pragma unroll
-    for (u32 k = 0; k < 4; ++k) W[k] *= 2u;
-#pragma unroll
-    for (u32 j = 0; j < 16; ++j) {
-        const u32 w2 = (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
-        const u32 a = w2 ? sbase + o2 + ((o2 >> 3) & ~3u) : trash_addr;
-        auto* p = reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(a);
-        if (j & 1u) *p = (uint16_t)((((o2 << 23) & 0x0F000000u) | xk[j >> 1]) >> 16);
-        else *p = (uint16_t)(((o2 << 7) & 0x0F00u) | xk[j >> 1]);
-        o2 += w2;
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 nsb = nib_to_bytes(bfe(NS, 4u * k, 4));
+        const u32 val = (prevw[k] & (nsb * 0xFFu)) | (w[k] & ~(nsb * 0xFFu));
+        const u32 xk_lo = __builtin_amdgcn_perm(0x01010101u, val, 0x04010400u);
+        const u32 xk_hi = __builtin_amdgcn_perm(0x01010101u, val, 0x04030402u);
+        const u32 W2 = ln.W[k] << 1;
+        u32 P = W2 + (W2 << 8);
+        P += P << 16;                                             // inclusive byte prefix
+        const u32 X = (P << 8) + 0x02020202u - 2u * nsb;           // exclusive, -2 at interior positions
+        dec_scatter4(base, X, xk_lo, xk_hi);
+        base += P >> 24;
     }
     wave_lds_sync();
     RLE_STAMP(st.sp, 2);   // scatter
@@ -648,17 +685,20 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
     const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
-    if (nfl) {   // move the partial chunk to staging chunk 1
+    if (nfl) {   // move the partial chunk to staging chunk 1 (tags follow the position: bit 4 flips with nfl)
         if (lane < 8u) {
             u32* s32 = reinterpret_cast<u32*>(stage);
-            s32[9u + lane] = s32[9u * (nfl + 1u) + lane];
-            s32[9u * (nfl + 1u) + lane] = 0u;
+            u32 v = s32[8u * (nfl + 1u) + lane];
+            if (nfl & 1u) v ^= (v & 0x01000100u) << 7;
+            s32[8u + lane] = v;
+            s32[8u * (nfl + 1u) + lane] = 0u;
         }
         wave_lds_sync();
     }
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
     st.d = bfe(readlane(incl, 63), 8u * st.d, 8);
+    st.prev = readlane(w[3], kOwnLanes - 1u);
     RLE_STAMP(st.sp, 7);   // partial-chunk move, state
     return rounds;
 }
@@ -672,7 +712,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
     const u32 span = end - st.flushed;
     const u32 nq = (span + 15u) >> 4;
     const u32 tv = st.tail & 0xFFu;
-    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stage + 36u);
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stage + 32u);
     for (u32 q0 = 0; q0 < nq; q0 += kWave) {
         const u32 q = q0 + lane;
         if (q < nq) {
@@ -682,7 +722,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
                 u32 v = tv;
                 if (q == 0u && j < rel) {
                     const u32 h = s16[j];
-                    cur = (h & 0x8000u) ? (h & 0xFFu) : cur;
+                    cur = (h & kKeyFlag) ? (h & 0xFFu) : cur;
                     v = cur;
                 }
                 ob[j >> 2] |= v << (8u * (j & 3u));
@@ -699,7 +739,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
         }
     }
     wave_lds_sync();
-    if (lane < 9u) reinterpret_cast<u32*>(stage)[9u + lane] = 0u;   // staging chunk 1 back to zero
+    if (lane < 8u) reinterpret_cast<u32*>(stage)[8u + lane] = 0u;   // staging chunk 1 back to zero
     vm_drain();
 }
 

@@ -97,8 +97,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ out_cap,
                                                            uint32_t* __restrict__ status, uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
-    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kDecWaves * kDecStage];
-    __shared__ __attribute__((aligned(16))) uint16_t trash_all[kDecWaves * kWave];
+    __shared__ __attribute__((aligned(64))) uint8_t stage_all[kDecWaves * kDecStage];
     __shared__ DecEntry tbl[256];
 #ifdef RLE_LDS_PAD   // occupancy experiments only
     __shared__ uint8_t ldspad[RLE_LDS_PAD];
@@ -109,7 +108,6 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     for (u32 k = threadIdx.x; k < 256u; k += kDecBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
     uint8_t* stage = stage_all + wid * kDecStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    const u32 trash_addr = lds_addr(trash_all + wid * kWave + lane);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     if (kDecWaves > 1) __syncthreads();
@@ -131,13 +129,13 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         const u32 C = (u32)C64, U = (u32)U64;
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, {}};
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, {}};
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
         st.sp.last = memtime();
 #endif
         walk_tiles(rsi, 0u, ntiles_for(C), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, trash_addr, dst, rso, st);
+            return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st);
         });
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;

@@ -368,15 +368,13 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
                                                                   const uint2* __restrict__ plan,
                                                                   const u32* __restrict__ bflag) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
-    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kDecStage];
-    __shared__ __attribute__((aligned(16))) uint16_t trash_all[kSegWaves * kWave];
+    __shared__ __attribute__((aligned(64))) uint8_t stage_all[kSegWaves * kDecStage];
     __shared__ DecEntry tbl[256];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     for (u32 k = threadIdx.x; k < 256u; k += kSegBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
     uint8_t* stage = stage_all + wid * kDecStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    const u32 trash_addr = lds_addr(trash_all + wid * kWave + lane);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
@@ -404,9 +402,9 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         const u32 e = uniform(pl.x), off = uniform(pl.y);
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{off, off & ~15u, e, 0u, 0u, 0u, off & 15u, {}};
+        DecState st{off, off & ~15u, e, 0u, 0u, 0u, off & 15u, 0u, {}};
         walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, trash_addr, dst, rso, st);
+            return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st);
         });
         const bool last = g + 1u == s0 + nseg;
         dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);

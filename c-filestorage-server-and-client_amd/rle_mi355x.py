@@ -113,18 +113,19 @@ def decompress(stream: bytes, U: int, E: int = 0) -> bytes:
 
 
 # ------------------------------------------------------------------ batch layout helpers
-def layout(sizes, align=16):
-    """Offsets of buffers packed back to back, each start 16-byte aligned; returns (offs, total)."""
+def layout(sizes, align=16, pad=0):
+    """Offsets of buffers packed back to back, each start 16-byte aligned (plus `pad` spare bytes
+    after each buffer); returns (offs, total)."""
     offs, pos = [], 0
     for s in sizes:
         offs.append(pos)
-        pos += (int(s) + align - 1) // align * align
+        pos += (int(s) + align - 1) // align * align + pad
     return offs, max(pos, align)
 
 
-def compressed_slots(sizes):
+def compressed_slots(sizes, pad=0):
     """Worst-case-capacity output slots for encoding buffers of the given sizes."""
-    return layout([max_compressed_size(int(s)) for s in sizes])
+    return layout([max_compressed_size(int(s)) for s in sizes], pad=pad)
 
 
 def _ptr(t):
