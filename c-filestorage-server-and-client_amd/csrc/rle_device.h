@@ -108,6 +108,16 @@ __device__ __forceinline__ u32 bfe(u32 v, u32 off, u32 w) { return __builtin_amd
 __device__ __forceinline__ u32 bcnt(u32 v, u32 acc) { return (u32)__builtin_popcount(v) + acc; }
 // 4-bit mask -> bytes 0x01
 __device__ __forceinline__ u32 nib_to_bytes(u32 n) { return (n * 0x00204081u) & 0x01010101u; }
+// (a << s) + b in one full-rate op (left to itself the compiler folds a shift-add chain into a
+// quarter-rate v_mul_lo_u32)
+template <int kShift>
+__device__ __forceinline__ u32 lshl_add(u32 a, u32 b) {
+    u32 r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(kShift), "v"(b));
+    return r;
+}
+// 0xFF in every byte that is non-zero in m (bytes of m in 0..3: v_perm selectors 0x0C -> 0x00, 0x0D.. -> 0xFF)
+__device__ __forceinline__ u32 bytes_ff(u32 m) { return __builtin_amdgcn_perm(0u, 0u, m | 0x0C0C0C0Cu); }
 __device__ __forceinline__ u32 mod9(u32 x) {
     const u32 q = __umulhi(x, 0x38E38E39u) >> 1;
     return x - 9u * q;
@@ -399,15 +409,52 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
 }
 
 // ================================================================ DECODE
-// Token-phase table: for an 8-bit mask e of "byte j equals byte j+1" and entry offset d (the
-// first token start in the group, 0..2): .x byte d = token-start mask, .y byte d = offset of the
-// first start past the group (.y byte 3 = 3, so .y is a v_perm selector).
+#ifndef RLE_ABL   // ablation builds (timing only, wrong output): 1 no phase scan, 2 no scatter, 4 no fill, 8 scatter without its LDS writes
+#define RLE_ABL 0
+#endif
+// Instruction selection (measured, tools/probes/valu_rate_probe.hip, gfx950): v_add/v_sub/v_and/
+// v_or/v_xor/v_lshrrev/v_not and v_bitop3 with VGPR or literal operands issue at ~1.9 cycles per
+// wave-instruction with 4 waves per SIMD; everything else the codec uses (v_perm, v_alignbyte,
+// v_bfe, v_lshlrev, v_mul*, v_dot4, SDWA, DPP, v_pk_*, v_and_or/v_lshl_or/v_add3, and ANY op with an
+// SGPR operand) at ~3.  So the SWAR below keeps masks in 0x80-per-byte form (derived with right
+// shifts), folds logic into v_bitop3 with constants held in VGPRs (vconst), and leaves the slow
+// forms to the few places they replace several fast ops.
+__device__ __forceinline__ u32 vconst(u32 c) {
+    u32 r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
+    return r;
+}
+template <u32 kImm>
+__device__ __forceinline__ u32 bitop3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, kImm); }
+// Plain VOP2 forms.  (Inline asm for them would make the hazard recognizer put an s_nop after each;
+// the SDWA peephole that would fold them into slow-class byte/word-select adds is disabled for
+// this code in the Makefile: -mllvm -amdgpu-sdwa-peephole=0.)
+__device__ __forceinline__ u32 fadd(u32 a, u32 b) { return a + b; }
+__device__ __forceinline__ u32 fsub(u32 a, u32 b) { return a - b; }
+template <u32 kImm>
+__device__ __forceinline__ u32 faddi(u32 a) { return a + kImm; }
+template <u32 kImm>
+__device__ __forceinline__ u32 fandi(u32 a) { return a & kImm; }
+template <u32 kSh>
+__device__ __forceinline__ u32 fshr(u32 a) { return a >> kSh; }
+// bitop3 truth-table immediates (inputs a = 0xF0, b = 0xCC, c = 0xAA)
+constexpr u32 kOrAnd = (0xF0 | 0xCC) & 0xAA;          // (a | b) & c
+constexpr u32 kAndNot = 0xF0 & ~0xCC & 0xFF;          // a & ~b
+constexpr u32 kSel = ((0xF0 & 0xAA) | (0xCC & ~0xAA)) & 0xFF;   // c ? a : b (bitwise)
+constexpr u32 kBad = ((0xF0 | (~0xCC) | 0xAA)) & 0xFF;          // a | ~b | c
+constexpr u32 kAndOr = ((0xF0 & 0xCC) | 0xAA) & 0xFF;           // (a & b) | c
+
+// Token-phase table, indexed by an 8-bit mask n of "byte j differs from byte j+1" (the complement
+// of the 3-byte-token mask) and entry offset d (the first token start in the group, 0..2):
+// .x byte d = token-start mask, .y byte d = offset of the first start past the group (.y byte 3
+// = 3, so .y is a v_perm selector).
 struct DecTable {
     uint2 e[256];
 };
 constexpr DecTable make_dec_table() {
     DecTable t{};
-    for (u32 e = 0; e < 256; ++e) {
+    for (u32 n = 0; n < 256; ++n) {
+        const u32 e = ~n & 0xFFu;
         u32 masks = 0, exits = 3u << 24;
         for (u32 d = 0; d < 3; ++d) {
             u32 s = d, m = 0;
@@ -418,49 +465,33 @@ constexpr DecTable make_dec_table() {
             masks |= m << (8u * d);
             exits |= (s - 8u) << (8u * d);
         }
-        t.e[e].x = masks;
-        t.e[e].y = exits;
+        t.e[n].x = masks;
+        t.e[n].y = exits;
     }
     return t;
 }
 static __constant__ DecTable kDecTable = make_dec_table();
-#ifndef RLE_DEC_TBL32
-#define RLE_DEC_TBL32 0
-#endif
-// packed form (1 KiB): bits 0..23 = the three masks, bits 24+2d = exit offset from entry d
-#if RLE_DEC_TBL32
-typedef u32 DecEntry;
-__device__ __forceinline__ DecEntry dec_entry_from(uint2 e) {
-    return (e.x & 0xFFFFFFu) | ((e.y & 3u) << 24) | (((e.y >> 8) & 3u) << 26) | (((e.y >> 16) & 3u) << 28);
-}
-__device__ __forceinline__ u32 ent_masks(DecEntry e) { return e; }
-__device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e, 24u + 2u * d, 2); }
-__device__ __forceinline__ u32 ent_sel(DecEntry e) {
-    const u32 x = e >> 24;
-    return (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | 0x03000000u;
-}
-#else
 typedef uint2 DecEntry;
 __device__ __forceinline__ DecEntry dec_entry_from(uint2 e) { return e; }
-__device__ __forceinline__ u32 ent_masks(DecEntry e) { return e.x; }
-__device__ __forceinline__ u32 ent_exit(DecEntry e, u32 d) { return bfe(e.y, 8u * d, 8); }
-__device__ __forceinline__ u32 ent_sel(DecEntry e) { return e.y; }
-#endif
+__device__ __forceinline__ DecEntry lds_entry(u32 a) {
+    typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x2*>(a);
+    return make_uint2(v.x, v.y);
+}
 
 // Staging (per wave): decoded position r (biased by 16: chunk 0 is a guard, never stored) holds a
-// u16 key: 0 = empty, else (r & 31) << 11 | 0x100 | byte.  Chunk c is the 32 bytes at 32 c (no
-// padding: the flush reads and re-zeroes a chunk with two 16-byte accesses).  Within a 16-aligned
-// chunk the keys grow with position, so a packed-u16 prefix max fills each run from its key.
-// Every token start writes its key at its decoded position.  Every other valid position (the
-// second byte and the count digit of a 3-byte token) writes the key of the byte before it (which
-// is its token's byte) at the position before the running offset (its token's last decoded
-// position): a correct, redundant key, so no position needs a trash slot or a select.  Positions
-// past the owned range write at the running offset, past the tile's output; the next tile's first
-// key overwrites that slot.  A token decodes to at most 9 bytes, so every 16-byte chunk holds a
-// key, and the byte entering a chunk is the last key of the chunk before it.
-constexpr u32 kDecChunks = 192;              // >= ceil((16 + 15 + 3024 + 1) / 16)
-constexpr u32 kDecStage = 32u * kDecChunks;  // bytes per wave (a multiple of 64: tags = position & 31)
-constexpr u32 kKeyFlag = 0x100u;
+// u16 key: 0x80 << 8 | byte where a token starts, else 0 or an unflagged byte.  Chunk c is the 32
+// bytes at 32 c; the flush reads and re-zeroes a chunk with two 16-byte accesses and ORs each
+// position's index into bits 8..11, so that a packed-u16 prefix max fills each run from its key.
+// Every token start writes its key at its decoded position.  Every other owned position (the
+// second byte and the count digit of a 3-byte token) writes its byte, unflagged, at the position
+// before the running offset (its token's last decoded position, which holds no key: the tiled
+// path declines count digit '1'), so no position needs a trash slot or a select.  A token decodes
+// to at most 9 bytes, so every 16-byte chunk holds a key, and the byte entering a chunk is the
+// last key of the chunk before it.
+constexpr u32 kDecChunks = 192;              // >= ceil((16 + 15 + 3024 + 1) / 16): a tile decodes to <= 3024 B
+constexpr u32 kDecStage = 32u * kDecChunks;  // bytes per wave
+constexpr u32 kKeyFlag = 0x8000u;
 
 struct DecState {
     u32 out_pos;   // decoded bytes produced so far
@@ -474,18 +505,18 @@ struct DecState {
     Stamps sp;     // diagnostic builds only
 };
 
-// v + byte k of x (one SDWA add)
+// v - byte k of x (one SDWA subtract)
 template <int kByte>
-__device__ __forceinline__ u32 add_byte(u32 v, u32 x) {
+__device__ __forceinline__ u32 sub_byte(u32 v, u32 x) {
     u32 r;
     if constexpr (kByte == 0)
-        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(v), "v"(x));
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(v), "v"(x));
     else if constexpr (kByte == 1)
-        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(v), "v"(x));
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(v), "v"(x));
     else if constexpr (kByte == 2)
-        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(v), "v"(x));
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(v), "v"(x));
     else
-        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(v), "v"(x));
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(v), "v"(x));
     return r;
 }
 
@@ -503,20 +534,26 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
             b = s4[1];
         }
         RLE_STAMP(sp, 3);   // flush: staging reads
-        u32 L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        // position index p (bits 8..11 of each u16) into each key; empty slots get the index alone,
+        // below every key and below the carry
+        u32 L[8] = {a.x | 0x01000000u, a.y | 0x03000200u, a.z | 0x05000400u, a.w | 0x07000600u,
+                    b.x | 0x09000800u, b.y | 0x0B000A00u, b.z | 0x0D000C00u, b.w | 0x0F000E00u};
         // prefix max of the keys inside the chunk: within each pair, then across pairs
+        if (!(RLE_ABL & 4)) {
 #pragma unroll
-        for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
+            for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
 #pragma unroll
-        for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m - 1], L[m - 1], 0x03020302u));
-        const u32 lastb = bfe(L[7], 16, 8);   // byte of the chunk's last key = its last output byte
+            for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m - 1], L[m - 1], 0x03020302u));
+        }
+        const u32 lastb = (L[7] >> 16) & 0xFFu;   // byte of the chunk's last key = its last output byte
         const u32 carry = from_prev_lane(lastb, fillc);
-        const u32 crep = carry * 0x00010001u;
+        // a run entering the chunk covers at most its first 8 positions (dwords 0..3)
+        const u32 crep = carry | 0x10001000u | (carry << 16);
         u32x4 o;
         o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
         o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
-        o.z = __builtin_amdgcn_perm(pkmax(L[5], crep), pkmax(L[4], crep), 0x06040200u);
-        o.w = __builtin_amdgcn_perm(pkmax(L[7], crep), pkmax(L[6], crep), 0x06040200u);
+        o.z = __builtin_amdgcn_perm(L[5], L[4], 0x06040200u);
+        o.w = __builtin_amdgcn_perm(L[7], L[6], 0x06040200u);
         RLE_STAMP(sp, 4);   // flush: fill + carry
         const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
         vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o);   // RLE_NOSTORE: diagnostic
@@ -539,99 +576,132 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
 }
 
 // Decode tile analysis (shared by dec_tile and the segment summary).  dec_prepare: the tile's
-// bytes (zero past C), the E mask (y[j] == y[j+1]: a token starting at j is 3 bytes long) and the
-// wave scan of the lanes' token-phase maps.  Positions are absolute in the stream; tokens start
-// only below Co (the end of the positions this wave owns: the stream, or its segment).
+// bytes (zero past C), the per-byte "differs from the next byte" flags g (0x80 per byte: a token
+// starting there is 1 byte long), their bit masks, and the wave scan of the lanes' token-phase
+// maps.  Positions are absolute in the stream; tokens start only below Co (the end of the
+// positions this wave owns: the stream, or its segment).  Lane 63 holds only the next tile's first
+// 16 bytes (lookahead): its results are garbage and every consumer ignores it.
 struct DecPrep {
-    u32 w[4];
-    u32 la, left, validm, E, incl, excl;
+    u32 w[4], g[4];
+    u32 la;        // next lane's first 4 bytes (count digits of positions 14, 15)
+    u32 left;      // stream bytes from the lane's first position
+    u32 lefto;     // owned positions from the lane's first position
+    u32 xa, xb;    // NE bits of positions 0..7 / 8..15, at bits 7..14
+    u32 incl, excl;
     DecEntry ta, tb;
+    bool tail;     // the tile reaches the owned end or the stream end (validity masks needed)
 };
 __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, u32 Co, u32 lane,
                                                const DecEntry* tbl) {
     DecPrep r;
     const u32 p0 = pos + 16u * lane;
-    const u32 left = p0 < C ? C - p0 : 0u;
-    r.left = left;
-    const u32 nl = left < 16u ? left : 16u;
-    const u32 lefto = p0 < Co ? Co - p0 : 0u;
-    r.validm = lane < kOwnLanes ? lowmask(lefto < 16u ? lefto : 16u) : 0u;
+    r.left = p0 < C ? C - p0 : 0u;
+    r.lefto = p0 < Co ? Co - p0 : 0u;
+    r.tail = pos + kSlot + 2u > Co;   // (Co <= C) positions >= Co or digits past C occur only here
     u32* w = r.w;
     w[0] = cur.x; w[1] = cur.y; w[2] = cur.z; w[3] = cur.w;
     if (pos + kSlot > C) {   // last tiles: bytes at index >= C read as the stream's zero padding
+        const u32 nl = r.left < 16u ? r.left : 16u;
 #pragma unroll
         for (u32 k = 0; k < 4; ++k) {
             const u32 nb = nl > 4u * k ? (nl - 4u * k < 4u ? nl - 4u * k : 4u) : 0u;
             w[k] &= lowmask(8u * nb);
         }
     }
-    const u32 la = from_next_lane(w[0] & 0xFFFFu, 0u) & 0xFFFFu;   // 2-byte lookahead
+    const u32 la = from_next_lane(w[0], 0u);
     r.la = la;
-    const u32 NE = nz4(w[0] ^ alignbyte(w[1], w[0], 1)) | (nz4(w[1] ^ alignbyte(w[2], w[1], 1)) << 4) |
-                   (nz4(w[2] ^ alignbyte(w[3], w[2], 1)) << 8) | (nz4(w[3] ^ alignbyte(la, w[3], 1)) << 12);
-    r.E = ~NE & 0xFFFFu;
-    r.ta = tbl[r.E & 0xFFu];
-    r.tb = tbl[r.E >> 8];
-    const u32 selb = ent_sel(r.tb);
-    const u32 map = lane < kOwnLanes ? __builtin_amdgcn_perm(selb, selb, ent_sel(r.ta)) : kMapId;
-    r.incl = wave_scan_incl(map, kMapId, OpMap());
+    const u32 K80 = vconst(0x80808080u);
+    const u32 nx[4] = {alignbyte(w[1], w[0], 1), alignbyte(w[2], w[1], 1), alignbyte(w[3], w[2], 1),
+                       alignbyte(la, w[3], 1)};
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 t = w[k] ^ nx[k];
+        const u32 u = faddi<0x7F7F7F7Fu>(fandi<0x7F7F7F7Fu>(t));
+        r.g[k] = bitop3<kOrAnd>(u, t, K80);
+    }
+    const u32 C1 = vconst(0x08040201u), C2 = vconst(0x80402010u);
+    r.xa = __builtin_amdgcn_udot4(r.g[1], C2, __builtin_amdgcn_udot4(r.g[0], C1, 0u, false), false);
+    r.xb = __builtin_amdgcn_udot4(r.g[3], C2, __builtin_amdgcn_udot4(r.g[2], C1, 0u, false), false);
+    const u32 tbase = lds_addr(tbl);
+    r.ta = lds_entry(tbase + (r.xa >> 4));
+    r.tb = lds_entry(tbase + (r.xb >> 4));
+    const u32 map = __builtin_amdgcn_perm(r.tb.y, r.tb.y, r.ta.y);
+    r.incl = (RLE_ABL & 1) ? map : wave_scan_incl(map, kMapId, OpMap());
     r.excl = from_prev_lane(r.incl, kMapId);
     return r;
 }
-// dec_lengths: for tile-entry phase d, the token starts S, pair starts P (MP: count digit inside
-// the stream, PF: digit in the zero padding = the stream's final token), decoded length per
-// position W (bytes), the lane's decoded byte count and whether the tiled path must decline.
-// Digits '1'..'9' give d-'0'; anything else -> serial path.
+// dec_lengths: for tile-entry phase d, the token-start bytes S01 (1 per start), the decoded length
+// per position W (bytes), the lane's decoded byte count and whether the tiled path must decline
+// (a count digit outside '1'..'9'); tail tiles also mask positions past the owned range and
+// report PF (bits): pair starts whose count digit lies in the zero padding (the stream's final,
+// unbounded token).
 struct DecLen {
-    u32 S, PF, nout;
-    u32 W[4];
+    u32 W[4], S01[4], S80[4], N01[4];   // N01: owned positions that are not token starts
+    u32 nout, PF;
     bool serial_lane;
 };
+// 16-bit mask -> 0x80 per byte for the 4 positions of dword k ((nibble << 7) * 0x00204081 puts
+// bit i at bit 8 i + 7)
+__device__ __forceinline__ u32 expand80(u32 m16, u32 k, u32 K80) {
+    return __umul24(bfe(m16, 4u * k, 4) << 7, 0x00204081u) & K80;
+}
 __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     DecLen r;
     const u32* w = p.w;
-    const u32 dl = bfe(p.excl, 8u * d, 8);
-    const u32 mid = ent_exit(p.ta, dl);
-    const u32 S = (bfe(ent_masks(p.ta), 8u * dl, 8) | (bfe(ent_masks(p.tb), 8u * mid, 8) << 8)) & p.validm;
-    r.S = S;
-    const u32 P = S & p.E;
-    const u32 left18 = p.left < 18u ? p.left : 18u;
-    const u32 v18 = lowmask(left18);
-    const u32 MP = P & (v18 >> 2);
-    const u32 PF = P & ~(v18 >> 2);
-    r.PF = PF;
+    const u32 dl = bfe(p.excl, 8u * d, 8);                                    // lane entry phase
+    const u32 mid = __builtin_amdgcn_perm(0u, p.ta.y, 0x0C0C0C00u | dl);      // phase entering position 8
+    const u32 sa = __builtin_amdgcn_perm(0u, p.ta.x, 0x0C0C0C00u | dl);       // start bits 0..7
+    const u32 sb = __builtin_amdgcn_perm(0u, p.tb.x, 0x0C0C0C00u | mid);      // start bits 8..15
+    const u32 K80 = vconst(0x80808080u);
+    const u32 sa7 = sa << 7, sb7 = sb << 7;
+    u32 S80[4] = {__umul24(sa7 & 0x780u, 0x00204081u) & K80,
+                  __umul24((sa7 >> 4) & 0x780u, 0x00204081u) & K80,
+                  __umul24(sb7 & 0x780u, 0x00204081u) & K80,
+                  __umul24((sb7 >> 4) & 0x780u, 0x00204081u) & K80};
     const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
                        alignbyte(p.la, w[3], 2)};
-    u32 extra = 0, badb = 0;
+    u32 VD80[4] = {K80, K80, K80, K80};   // positions whose count digit lies inside the stream
+    u32 O01[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};   // owned positions
+    r.PF = 0u;
+    bool sf = false;
+    if (p.tail) {
+        // owned: j < lefto; digit inside the stream: j + 2 < left; second byte inside: j + 1 < left
+        const u32 lo16 = lowmask(p.lefto < 16u ? p.lefto : 16u);
+        const u32 l18 = lowmask(p.left < 18u ? p.left : 18u);
+        const u32 S16 = (sa | (sb << 8)) & lo16;
+        const u32 NE16 = (p.xa >> 7) | (p.xb << 1);
+        r.PF = S16 & ~NE16 & ~(l18 >> 2) & 0xFFFFu;   // pair starts whose digit is past C
+        sf = (r.PF & (l18 >> 1)) != 0u;                // ... while the second byte is not: decline
+#pragma unroll
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 vo = expand80(lo16, k, K80);
+            S80[k] &= vo;
+            O01[k] = vo >> 7;
+            VD80[k] = expand80(l18 >> 2, k, K80);
+        }
+    }
+    u32 bad = 0u, sum = 0u;
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
-        const u32 mpb = nib_to_bytes(bfe(MP, 4u * k, 4));
-        const u32 dor = dg[k] | 0x80808080u;
-        const u32 lo = dor - 0x31313131u, hi = dor - 0x3A3A3A3Au;
-        const u32 dm1 = lo & 0x7F7F7F7Fu & ((mpb << 8) - mpb);   // d - '1' at pair starts
-        extra = __builtin_amdgcn_udot4(dm1, 0x01010101u, extra, false);
-        badb |= (~lo | hi | dg[k]) & (mpb << 7);
-        r.W[k] = nib_to_bytes(bfe(S, 4u * k, 4)) + dm1;        // decoded length per position
+        const u32 P80 = bitop3<0xF0 & ~0xCC & 0xAA>(S80[k], p.g[k], VD80[k]);   // 3-byte start, digit in stream
+        const u32 P7F = fsub(P80, fshr<7>(P80));
+        const u32 xm = fandi<0x7F7F7F7Fu>(dg[k]);
+        const u32 a = faddi<0x46464646u>(xm);   // bit 7: digit >= ':'
+        const u32 b2 = faddi<0x4E4E4E4Eu>(xm);  // bit 7: digit >= '2'
+        const u32 b = faddi<0x4F4F4F4Fu>(xm);   // low 7 bits: digit - '1'
+        bad = bitop3<kAndOr>(bitop3<kBad>(a, b2, dg[k]), P80, bad);
+        const u32 S01 = fshr<7>(S80[k]);
+        r.S80[k] = S80[k];
+        r.S01[k] = S01;
+        r.N01[k] = fsub(O01[k], S01);
+        r.W[k] = fadd(S01, b & P7F);
+        sum = fadd(sum, r.W[k]);
     }
-    r.nout = bcnt(S, extra);
-    r.serial_lane = badb != 0u || (PF & (v18 >> 1)) != 0u;
+    sum = fadd(sum, fshr<16>(sum));
+    sum = fadd(sum, fshr<8>(sum));
+    r.nout = fandi<0xFFu>(sum);
+    r.serial_lane = (bad & K80) != 0u || sf;
     return r;
-}
-
-// Scatter one dword's four positions: position 4k+i writes key(t) at staging byte address t =
-// base + byte i of X (X: the exclusive byte prefix of the doubled lengths, +2 for starts and
-// past-range positions, +0 for token-interior positions).
-template <int kHalf>
-__device__ __forceinline__ void dec_put(u32 t, u32 xk) {
-    auto* p = reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(t);
-    if constexpr (kHalf == 0) *p = (uint16_t)((t << 10) | xk);
-    else *p = (uint16_t)(((t << 26) | xk) >> 16);
-}
-__device__ __forceinline__ void dec_scatter4(u32 base, u32 X, u32 xk_lo, u32 xk_hi) {
-    dec_put<0>(add_byte<0>(base, X), xk_lo);
-    dec_put<1>(add_byte<1>(base, X), xk_lo);
-    dec_put<0>(add_byte<2>(base, X), xk_hi);
-    dec_put<1>(add_byte<3>(base, X), xk_hi);
 }
 
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
@@ -643,41 +713,47 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl);
     const DecLen ln = dec_lengths(pr, st.d);
     const u32* w = pr.w;
-    const u32 incl = pr.incl, PF = ln.PF, nout = ln.nout;
-    const bool serial_lane = ln.serial_lane;
-    const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
-    const u32 ttot = readlane(oincl, 63);
-    if (__builtin_amdgcn_ballot_w64(serial_lane) || st.out_pos + ttot > U) {
+    const u32 oincl = wave_scan_incl(ln.nout, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, kOwnLanes - 1u);
+    constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+    if ((__builtin_amdgcn_ballot_w64(ln.serial_lane) & kOwned) || st.out_pos + ttot > U) {
         st.serial = 1;
         return ~0u;
     }
-    const uint64_t pfb = __builtin_amdgcn_ballot_w64(PF != 0u);
-    if (pfb) {   // the final token's byte extends to U
-        const u32 jf = (u32)__builtin_ctz(PF | 0x10000u) & 15u;
-        const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
-        st.tail = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+    if (pr.tail) {
+        const uint64_t pfb = __builtin_amdgcn_ballot_w64(ln.PF != 0u) & kOwned;
+        if (pfb) {   // the final token's byte extends to U
+            const u32 jf = (u32)__builtin_ctz(ln.PF | 0x10000u) & 15u;
+            const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
+            st.tail = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+        }
     }
 
     RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
-    // key values: a start's own byte, an interior position's previous byte (its token's byte)
-    const u32 NS = pr.validm & ~ln.S;
-    const u32 ptop = from_prev_lane(w[3], st.prev);
-    const u32 prevw[4] = {alignbyte(w[0], ptop, 3), alignbyte(w[1], w[0], 3), alignbyte(w[2], w[1], 3),
-                          alignbyte(w[3], w[2], 3)};
     const u32 rel0 = st.out_pos - st.flushed;
-    u32 base = lds_addr(stage) + 2u * (16u + rel0 + oincl - nout) - 2u;
+    // staging byte address after this lane's output (2 B per decoded position)
+    u32 endk = lds_addr(stage) + 2u * (16u + rel0 + oincl - ln.nout);
+    if (lane < kOwnLanes && !(RLE_ABL & 2)) {
 #pragma unroll
-    for (u32 k = 0; k < 4; ++k) {
-        const u32 nsb = nib_to_bytes(bfe(NS, 4u * k, 4));
-        const u32 val = (prevw[k] & (nsb * 0xFFu)) | (w[k] & ~(nsb * 0xFFu));
-        const u32 xk_lo = __builtin_amdgcn_perm(0x01010101u, val, 0x04010400u);
-        const u32 xk_hi = __builtin_amdgcn_perm(0x01010101u, val, 0x04030402u);
-        const u32 W2 = ln.W[k] << 1;
-        u32 P = W2 + (W2 << 8);
-        P += P << 16;                                             // inclusive byte prefix
-        const u32 X = (P << 8) + 0x02020202u - 2u * nsb;           // exclusive, -2 at interior positions
-        dec_scatter4(base, X, xk_lo, xk_hi);
-        base += P >> 24;
+        for (u32 k = 0; k < 4; ++k) {
+            // u16 per position: the byte, with the start flag (0x80) as the high byte: 0x80vv at a
+            // token start, an unflagged 0x00vv (ignored by the fill) anywhere else
+            const u32 xk_lo = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x05010400u);
+            const u32 xk_hi = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x07030602u);
+            const u32 W2 = fadd(ln.W[k], ln.W[k]);
+            u32 Q = fadd(W2, fshr<8>(W2));
+            Q = fadd(Q, fshr<16>(Q));                        // byte i: sum of W2 over positions >= i
+            endk = fadd(endk, fandi<0xFFu>(Q));              // staging address after the dword's output
+            const u32 R = fadd(Q, fadd(ln.N01[k], ln.N01[k]));   // interior positions: one slot further back
+            auto put = [](u32 t, u32 key) {
+                if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
+                else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(t) = (uint16_t)key;
+            };
+            put(sub_byte<0>(endk, R), xk_lo);
+            put(sub_byte<1>(endk, R), xk_lo >> 16);
+            put(sub_byte<2>(endk, R), xk_hi);
+            put(sub_byte<3>(endk, R), xk_hi >> 16);
+        }
     }
     wave_lds_sync();
     RLE_STAMP(st.sp, 2);   // scatter
@@ -685,19 +761,17 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
     const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
-    if (nfl) {   // move the partial chunk to staging chunk 1 (tags follow the position: bit 4 flips with nfl)
+    if (nfl) {   // move the partial chunk to staging chunk 1
         if (lane < 8u) {
             u32* s32 = reinterpret_cast<u32*>(stage);
-            u32 v = s32[8u * (nfl + 1u) + lane];
-            if (nfl & 1u) v ^= (v & 0x01000100u) << 7;
-            s32[8u + lane] = v;
+            s32[8u + lane] = s32[8u * (nfl + 1u) + lane];
             s32[8u * (nfl + 1u) + lane] = 0u;
         }
         wave_lds_sync();
     }
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
-    st.d = bfe(readlane(incl, 63), 8u * st.d, 8);
+    st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
     st.prev = readlane(w[3], kOwnLanes - 1u);
     RLE_STAMP(st.sp, 7);   // partial-chunk move, state
     return rounds;
@@ -712,7 +786,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
     const u32 span = end - st.flushed;
     const u32 nq = (span + 15u) >> 4;
     const u32 tv = st.tail & 0xFFu;
-    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stage + 32u);
+    const u32 c1 = lds_addr(stage) + 32u;   // staging chunk 1
     for (u32 q0 = 0; q0 < nq; q0 += kWave) {
         const u32 q = q0 + lane;
         if (q < nq) {
@@ -721,7 +795,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
             for (u32 j = 0; j < 16u; ++j) {
                 u32 v = tv;
                 if (q == 0u && j < rel) {
-                    const u32 h = s16[j];
+                    const u32 h = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(c1 + 2u * j);
                     cur = (h & kKeyFlag) ? (h & 0xFFu) : cur;
                     v = cur;
                 }

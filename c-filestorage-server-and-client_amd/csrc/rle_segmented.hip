@@ -83,6 +83,11 @@ __device__ __forceinline__ void seg_range(u32 i, u32 nseg, u32 n, u32 sb, u32& p
 }
 
 __device__ __forceinline__ u32 wave_sum(u32 x) { return readlane(wave_scan_incl(x, 0u, OpAdd()), 63); }
+// over the tile-owning lanes 0..62 (lane 63 holds the lookahead only)
+__device__ __forceinline__ u32 owned_sum(u32 x) { return readlane(wave_scan_incl(x, 0u, OpAdd()), kOwnLanes - 1u); }
+__device__ __forceinline__ bool owned_any(bool x) {
+    return (__builtin_amdgcn_ballot_w64(x) & ((1ull << kOwnLanes) - 1ull)) != 0ull;
+}
 
 // ================================================================ ENCODE
 // compressed bytes of the tokens starting in a segment's entering run piece (length L0) when the
@@ -274,24 +279,24 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_
                 const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
                 nx();
                 const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl);
-                const u32 m63 = readlane(pr.incl, 63);
+                const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
                 if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
                     const DecLen ln = dec_lengths(pr, d0);
-                    const u32 tot = wave_sum(ln.nout);
-                    const bool bad = __builtin_amdgcn_ballot_w64(ln.serial_lane) != 0;
+                    const u32 tot = owned_sum(ln.nout);
+                    const bool bad = owned_any(ln.serial_lane);
                     c0 += tot; c1 += tot; c2 += tot;
                     badm |= bad ? 7u : 0u;
                     d0 = d1 = d2 = bfe(m63, 8u * d0, 8);
                 } else {
                     const DecLen l0 = dec_lengths(pr, d0);
-                    c0 += wave_sum(l0.nout);
-                    badm |= __builtin_amdgcn_ballot_w64(l0.serial_lane) ? 1u : 0u;
+                    c0 += owned_sum(l0.nout);
+                    badm |= owned_any(l0.serial_lane) ? 1u : 0u;
                     const DecLen l1 = dec_lengths(pr, d1);
-                    c1 += wave_sum(l1.nout);
-                    badm |= __builtin_amdgcn_ballot_w64(l1.serial_lane) ? 2u : 0u;
+                    c1 += owned_sum(l1.nout);
+                    badm |= owned_any(l1.serial_lane) ? 2u : 0u;
                     const DecLen l2 = dec_lengths(pr, d2);
-                    c2 += wave_sum(l2.nout);
-                    badm |= __builtin_amdgcn_ballot_w64(l2.serial_lane) ? 4u : 0u;
+                    c2 += owned_sum(l2.nout);
+                    badm |= owned_any(l2.serial_lane) ? 4u : 0u;
                     d0 = bfe(m63, 8u * d0, 8);
                     d1 = bfe(m63, 8u * d1, 8);
                     d2 = bfe(m63, 8u * d2, 8);
