@@ -257,6 +257,54 @@ struct Stamps {};
     } while (0)
 #endif
 
+// ================================================================ fast-op helpers
+// Instruction selection (measured, tools/probes/valu_rate_probe.hip, gfx950): v_add/v_sub/v_and/
+// v_or/v_xor/v_lshrrev/v_not and v_bitop3 with VGPR or literal operands issue at ~1.9 cycles per
+// wave-instruction with 4 waves per SIMD; everything else the codec uses (v_perm, v_alignbyte,
+// v_bfe, v_lshlrev, v_mul*, v_dot4, SDWA, DPP, v_pk_*, v_and_or/v_lshl_or/v_add3, and ANY op with an
+// SGPR operand) at ~3.  So the SWAR below keeps masks in 0x80-per-byte form (derived with right
+// shifts), folds logic into v_bitop3 with constants held in VGPRs (vconst), and leaves the slow
+// forms to the few places they replace several fast ops.
+__device__ __forceinline__ u32 vconst(u32 c) {
+    u32 r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
+    return r;
+}
+template <u32 kImm>
+__device__ __forceinline__ u32 bitop3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, kImm); }
+// Plain VOP2 forms.  (Inline asm for them would make the hazard recognizer put an s_nop after each;
+// the SDWA peephole that would fold them into slow-class byte/word-select adds is disabled for
+// this code in the Makefile: -mllvm -amdgpu-sdwa-peephole=0.)
+__device__ __forceinline__ u32 fadd(u32 a, u32 b) { return a + b; }
+__device__ __forceinline__ u32 fsub(u32 a, u32 b) { return a - b; }
+template <u32 kImm>
+__device__ __forceinline__ u32 faddi(u32 a) { return a + kImm; }
+template <u32 kImm>
+__device__ __forceinline__ u32 fandi(u32 a) { return a & kImm; }
+template <u32 kSh>
+__device__ __forceinline__ u32 fshr(u32 a) { return a >> kSh; }
+// bitop3 truth-table immediates (inputs a = 0xF0, b = 0xCC, c = 0xAA)
+constexpr u32 kOrAnd = (0xF0 | 0xCC) & 0xAA;          // (a | b) & c
+constexpr u32 kAndNot = 0xF0 & ~0xCC & 0xFF;          // a & ~b
+constexpr u32 kSel = ((0xF0 & 0xAA) | (0xCC & ~0xAA)) & 0xFF;   // c ? a : b (bitwise)
+constexpr u32 kBad = ((0xF0 | (~0xCC) | 0xAA)) & 0xFF;          // a | ~b | c
+constexpr u32 kAndOr = ((0xF0 & 0xCC) | 0xAA) & 0xFF;           // (a & b) | c
+
+// v - byte k of x (one SDWA subtract)
+template <int kByte>
+__device__ __forceinline__ u32 sub_byte(u32 v, u32 x) {
+    u32 r;
+    if constexpr (kByte == 0)
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(v), "v"(x));
+    else if constexpr (kByte == 1)
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(v), "v"(x));
+    else if constexpr (kByte == 2)
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(v), "v"(x));
+    else
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(v), "v"(x));
+    return r;
+}
+
 // ================================================================ ENCODE
 // Staging (per wave): output position r of the tile (biased by 16: chunk 0 is a guard for the
 // back-writes of non-starts) lives at byte r.
@@ -297,8 +345,19 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
     const u32 top = w[3] & 0xFF000000u;
     a.top = top;
     const u32 ptop = from_prev_lane(top, prev_top);
-    u32 B = nz4(w[0] ^ alignbyte(w[0], ptop, 3)) | (nz4(w[1] ^ alignbyte(w[1], w[0], 3)) << 4) |
-            (nz4(w[2] ^ alignbyte(w[2], w[1], 3)) << 8) | (nz4(w[3] ^ alignbyte(w[3], w[2], 3)) << 12);
+    const u32 pw[4] = {alignbyte(w[0], ptop, 3), alignbyte(w[1], w[0], 3), alignbyte(w[2], w[1], 3),
+                       alignbyte(w[3], w[2], 3)};
+    const u32 K80 = vconst(0x80808080u);
+    u32 g[4];   // 0x80 per byte that differs from the byte before it
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 t = w[k] ^ pw[k];
+        g[k] = bitop3<kOrAnd>(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu), t, K80);
+    }
+    const u32 C1 = vconst(0x08040201u), C2 = vconst(0x80402010u);
+    const u32 Ba = __builtin_amdgcn_udot4(g[1], C2, __builtin_amdgcn_udot4(g[0], C1, 0u, false), false);
+    const u32 Bb = __builtin_amdgcn_udot4(g[3], C2, __builtin_amdgcn_udot4(g[2], C1, 0u, false), false);
+    u32 B = (Ba >> 7) | (Bb + Bb);
     B |= (p0 == 0u) ? 1u : 0u;
     B |= ~lowmask(nl) & 0xFFFFu;
     a.B = B;
@@ -345,23 +404,34 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     // at the tile's output end, which is never stored.  Per-position weights (T + 2P) and
     // back-offsets (2 for valid non-starts) are byte vectors.
     const u32 NS = validm & ~T;
-    u32 W[4], D[4];
+#ifndef RLE_EABL   // encode ablation builds (timing only): 1 no pass 1, 2 no pass 2, 4 no flush stores
+#define RLE_EABL 0
+#endif
+    // staging byte address after this lane's output; byte i of Q = output bytes of positions >= i
+    // of the dword (suffix sums by right shifts), so position i writes at endk - Q.byte_i (- 2)
+    u32 endk = lds_addr(stage) + 16u + rel0 + oincl - nout;
+    if (!(RLE_EABL & 1)) {
 #pragma unroll
-    for (u32 k = 0; k < 4; ++k) {
-        W[k] = nib_to_bytes(bfe(T, 4u * k, 4)) + 2u * nib_to_bytes(bfe(P, 4u * k, 4));
-        D[k] = 2u * nib_to_bytes(bfe(NS, 4u * k, 4));
-    }
-    u32 o = lds_addr(stage) + 16u + rel0 + oincl - nout;   // LDS byte address of the lane's output
-#pragma unroll
-    for (u32 j = 0; j < 16; ++j) {
-        const u32 a = o - ((D[j >> 2] >> (8u * (j & 3u))) & 0xFFu);
-        *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
-        o += (W[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 T01 = nib_to_bytes(bfe(T, 4u * k, 4)), P01 = nib_to_bytes(bfe(P, 4u * k, 4));
+            const u32 N01 = nib_to_bytes(bfe(NS, 4u * k, 4));
+            const u32 W = T01 + P01 + P01;
+            u32 Q = W + (W >> 8);
+            Q = Q + (Q >> 16);
+            endk = endk + (Q & 0xFFu);
+            const u32 R = Q + N01 + N01;
+            auto put = [](u32 t, u32 v) { *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(t) = (uint8_t)v; };
+            const u32 w8 = w[k] >> 8;
+            put(sub_byte<0>(endk, R), w[k]);
+            put(sub_byte<1>(endk, R), w8);
+            put(sub_byte<2>(endk, R), w[k] >> 16);
+            put(sub_byte<3>(endk, R), w8 >> 16);
+        }
     }
     RLE_STAMP(st.sp, 2);   // pass 1
     // pass 2: second byte and count digit of each 3-byte token, written from the token's own
     // tile (its second input byte may sit in the next tile, after this tile's flush)
-    u32 prem = P;
+    u32 prem = (RLE_EABL & 2) ? 0u : P;
     while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
         if (prem) {
             const u32 j = (u32)__builtin_ctz(prem);
@@ -386,7 +456,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
         u32x4 v = u32x4{0u, 0u, 0u, 0u};
         if (c < nfl) v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
         const bool skip = st.head && c == 0u;   // shared with the previous segment: byte stores below
-        vstore(rso, (c < nfl && !skip) ? st.flushed + 16u * c : kOOB, v);
+        vstore(rso, (c < nfl && !skip && !(RLE_EABL & 4)) ? st.flushed + 16u * c : kOOB, v);
         if (skip && nfl) {
             const u32 wv[4] = {v.x, v.y, v.z, v.w};
             for (u32 j = st.head; j < 16u; ++j) dst[st.flushed + j] = (uint8_t)(wv[j >> 2] >> (8u * (j & 3u)));
@@ -412,38 +482,6 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
 #ifndef RLE_ABL   // ablation builds (timing only, wrong output): 1 no phase scan, 2 no scatter, 4 no fill, 8 scatter without its LDS writes
 #define RLE_ABL 0
 #endif
-// Instruction selection (measured, tools/probes/valu_rate_probe.hip, gfx950): v_add/v_sub/v_and/
-// v_or/v_xor/v_lshrrev/v_not and v_bitop3 with VGPR or literal operands issue at ~1.9 cycles per
-// wave-instruction with 4 waves per SIMD; everything else the codec uses (v_perm, v_alignbyte,
-// v_bfe, v_lshlrev, v_mul*, v_dot4, SDWA, DPP, v_pk_*, v_and_or/v_lshl_or/v_add3, and ANY op with an
-// SGPR operand) at ~3.  So the SWAR below keeps masks in 0x80-per-byte form (derived with right
-// shifts), folds logic into v_bitop3 with constants held in VGPRs (vconst), and leaves the slow
-// forms to the few places they replace several fast ops.
-__device__ __forceinline__ u32 vconst(u32 c) {
-    u32 r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
-    return r;
-}
-template <u32 kImm>
-__device__ __forceinline__ u32 bitop3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, kImm); }
-// Plain VOP2 forms.  (Inline asm for them would make the hazard recognizer put an s_nop after each;
-// the SDWA peephole that would fold them into slow-class byte/word-select adds is disabled for
-// this code in the Makefile: -mllvm -amdgpu-sdwa-peephole=0.)
-__device__ __forceinline__ u32 fadd(u32 a, u32 b) { return a + b; }
-__device__ __forceinline__ u32 fsub(u32 a, u32 b) { return a - b; }
-template <u32 kImm>
-__device__ __forceinline__ u32 faddi(u32 a) { return a + kImm; }
-template <u32 kImm>
-__device__ __forceinline__ u32 fandi(u32 a) { return a & kImm; }
-template <u32 kSh>
-__device__ __forceinline__ u32 fshr(u32 a) { return a >> kSh; }
-// bitop3 truth-table immediates (inputs a = 0xF0, b = 0xCC, c = 0xAA)
-constexpr u32 kOrAnd = (0xF0 | 0xCC) & 0xAA;          // (a | b) & c
-constexpr u32 kAndNot = 0xF0 & ~0xCC & 0xFF;          // a & ~b
-constexpr u32 kSel = ((0xF0 & 0xAA) | (0xCC & ~0xAA)) & 0xFF;   // c ? a : b (bitwise)
-constexpr u32 kBad = ((0xF0 | (~0xCC) | 0xAA)) & 0xFF;          // a | ~b | c
-constexpr u32 kAndOr = ((0xF0 & 0xCC) | 0xAA) & 0xFF;           // (a & b) | c
-
 // Token-phase table, indexed by an 8-bit mask n of "byte j differs from byte j+1" (the complement
 // of the 3-byte-token mask) and entry offset d (the first token start in the group, 0..2):
 // .x byte d = token-start mask, .y byte d = offset of the first start past the group (.y byte 3
@@ -504,21 +542,6 @@ struct DecState {
     u32 prev;      // stream byte before the current tile, in bits 24..31
     Stamps sp;     // diagnostic builds only
 };
-
-// v - byte k of x (one SDWA subtract)
-template <int kByte>
-__device__ __forceinline__ u32 sub_byte(u32 v, u32 x) {
-    u32 r;
-    if constexpr (kByte == 0)
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(v), "v"(x));
-    else if constexpr (kByte == 1)
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(v), "v"(x));
-    else if constexpr (kByte == 2)
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(v), "v"(x));
-    else
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(v), "v"(x));
-    return r;
-}
 
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
