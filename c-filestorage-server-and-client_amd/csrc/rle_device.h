@@ -527,7 +527,10 @@ __device__ __forceinline__ DecEntry lds_entry(u32 a) {
 // path declines count digit '1'), so no position needs a trash slot or a select.  A token decodes
 // to at most 9 bytes, so every 16-byte chunk holds a key, and the byte entering a chunk is the
 // last key of the chunk before it.
-constexpr u32 kDecChunks = 192;              // >= ceil((16 + 15 + 3024 + 1) / 16): a tile decodes to <= 3024 B
+#ifndef RLE_DEC_CHUNKS   // (smaller values: occupancy experiments on random data only)
+#define RLE_DEC_CHUNKS 192
+#endif
+constexpr u32 kDecChunks = RLE_DEC_CHUNKS;   // >= ceil((16 + 15 + 3024 + 1) / 16): a tile decodes to <= 3024 B
 constexpr u32 kDecStage = 32u * kDecChunks;  // bytes per wave
 constexpr u32 kKeyFlag = 0x8000u;
 

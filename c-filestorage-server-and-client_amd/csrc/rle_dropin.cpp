@@ -72,9 +72,26 @@ struct Ctx {
     uint8_t* d_ws = nullptr;  size_t d_ws_cap = 0;    // segmented-path workspace
 };
 
+// A worker thread's context is released by its pthread-key destructor, which can still be running
+// when the process exits (a thread joined by its creator has not necessarily finished its TLS
+// destructors).  Process exit tears the HIP runtime down, so from the first atexit handler on no
+// context touches HIP any more (the OS reclaims the memory); the lock orders the two.
+pthread_mutex_t g_exit_lock = PTHREAD_MUTEX_INITIALIZER;
+bool g_exiting = false;
+void on_exit_handler() {
+    pthread_mutex_lock(&g_exit_lock);
+    g_exiting = true;
+    pthread_mutex_unlock(&g_exit_lock);
+}
+
 void free_ctx(void* p) {
     Ctx* c = static_cast<Ctx*>(p);
     if (!c) return;
+    pthread_mutex_lock(&g_exit_lock);
+    if (g_exiting) {
+        pthread_mutex_unlock(&g_exit_lock);
+        return;
+    }
     (void)hipSetDevice(c->dev);
     if (c->s) (void)hipStreamSynchronize(c->s);
     (void)hipHostFree(c->h_in);
@@ -86,12 +103,14 @@ void free_ctx(void* p) {
     (void)hipFree(c->d_ws);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
+    pthread_mutex_unlock(&g_exit_lock);
 }
 
 void init_once() {
     if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     pthread_key_create(&g_key, free_ctx);
+    atexit(on_exit_handler);   // registered after the HIP runtime's own exit hooks: runs before them
 }
 
 inline size_t round16(size_t x) { return (x + 15u) & ~(size_t)15u; }
