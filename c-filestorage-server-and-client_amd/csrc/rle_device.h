@@ -546,6 +546,14 @@ struct DecState {
     Stamps sp;     // diagnostic builds only
 };
 
+// Bank spread (RLE_SWZ): dword i of the staging chunk at byte address A (32-aligned) lives at
+// A + 4 (i ^ g), g = bits 7..9 of A.  A random-data tile decodes 16 positions (32 B) per lane and
+// a zero-fill tile 48 (96 B): unswizzled, each scatter write hits 4 of the 32 banks.
+#ifndef RLE_SWZ
+#define RLE_SWZ 0
+#endif
+__device__ __forceinline__ u32 sswz(u32 t) { return RLE_SWZ ? bitop3<0xF0 ^ (0xCC & 0xAA)>(t, t >> 5, 0x1Cu) : t; }
+
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
                                          u32& head, uint8_t* dst, Stamps& sp) {
@@ -556,8 +564,15 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         u32x4* s4 = reinterpret_cast<u32x4*>(stage + 32u * (c + 1u));
         u32x4 a = u32x4{0u, 0u, 0u, 0u}, b = a;
         if (active) {
-            a = s4[0];
-            b = s4[1];
+            if (RLE_SWZ) {
+                const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
+                auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
+                a = u32x4{rd(0), rd(1), rd(2), rd(3)};
+                b = u32x4{rd(4), rd(5), rd(6), rd(7)};
+            } else {
+                a = s4[0];
+                b = s4[1];
+            }
         }
         RLE_STAMP(sp, 3);   // flush: staging reads
         // position index p (bits 8..11 of each u16) into each key; empty slots get the index alone,
@@ -566,10 +581,13 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
                     b.x | 0x09000800u, b.y | 0x0B000A00u, b.z | 0x0D000C00u, b.w | 0x0F000E00u};
         // prefix max of the keys inside the chunk: within each pair, then across pairs
         if (!(RLE_ABL & 4)) {
+            // running max of the even positions (low halves) and of the odd ones (high halves) ...
 #pragma unroll
-            for (u32 m = 0; m < 8; ++m) L[m] = pkmax(L[m], L[m] << 16);
+            for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], L[m - 1]);
+            // ... then position 2m takes the odd max up to 2m-1, position 2m+1 the even max up to 2m
 #pragma unroll
-            for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m - 1], L[m - 1], 0x03020302u));
+            for (u32 m = 7; m > 0; --m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m], L[m - 1], 0x05040302u));
+            L[0] = pkmax(L[0], L[0] << 16);
         }
         const u32 lastb = (L[7] >> 16) & 0xFFu;   // byte of the chunk's last key = its last output byte
         const u32 carry = from_prev_lane(lastb, fillc);
@@ -639,10 +657,11 @@ __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, 
     const u32 K80 = vconst(0x80808080u);
     const u32 nx[4] = {alignbyte(w[1], w[0], 1), alignbyte(w[2], w[1], 1), alignbyte(w[3], w[2], 1),
                        alignbyte(la, w[3], 1)};
+    const u32 K7F = vconst(0x7F7F7F7Fu);   // in a VGPR: v_bitop3 with an SGPR operand is slow-class
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 t = w[k] ^ nx[k];
-        const u32 u = faddi<0x7F7F7F7Fu>(fandi<0x7F7F7F7Fu>(t));
+        const u32 u = faddi<0x7F7F7F7Fu>(t & K7F);
         r.g[k] = bitop3<kOrAnd>(u, t, K80);
     }
     const u32 C1 = vconst(0x08040201u), C2 = vconst(0x80402010u);
@@ -662,7 +681,7 @@ __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, 
 // report PF (bits): pair starts whose count digit lies in the zero padding (the stream's final,
 // unbounded token).
 struct DecLen {
-    u32 W[4], S01[4], S80[4], N01[4];   // N01: owned positions that are not token starts
+    u32 W[4], S01[4], S80[4], N02[4];   // N02: 2 at owned positions that are not token starts
     u32 nout, PF;
     bool serial_lane;
 };
@@ -687,7 +706,7 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
                        alignbyte(p.la, w[3], 2)};
     u32 VD80[4] = {K80, K80, K80, K80};   // positions whose count digit lies inside the stream
-    u32 O01[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};   // owned positions
+    u32 O02[4] = {0x02020202u, 0x02020202u, 0x02020202u, 0x02020202u};   // 2 at owned positions
     r.PF = 0u;
     bool sf = false;
     if (p.tail) {
@@ -702,7 +721,7 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
         for (u32 k = 0; k < 4; ++k) {
             const u32 vo = expand80(lo16, k, K80);
             S80[k] &= vo;
-            O01[k] = vo >> 7;
+            O02[k] = vo >> 6;
             VD80[k] = expand80(l18 >> 2, k, K80);
         }
     }
@@ -719,7 +738,7 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
         const u32 S01 = fshr<7>(S80[k]);
         r.S80[k] = S80[k];
         r.S01[k] = S01;
-        r.N01[k] = fsub(O01[k], S01);
+        r.N02[k] = fsub(O02[k], fshr<6>(S80[k]));
         r.W[k] = fadd(S01, b & P7F);
         sum = fadd(sum, r.W[k]);
     }
@@ -766,14 +785,14 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
             // token start, an unflagged 0x00vv (ignored by the fill) anywhere else
             const u32 xk_lo = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x05010400u);
             const u32 xk_hi = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x07030602u);
-            const u32 W2 = fadd(ln.W[k], ln.W[k]);
-            u32 Q = fadd(W2, fshr<8>(W2));
-            Q = fadd(Q, fshr<16>(Q));                        // byte i: sum of W2 over positions >= i
+            u32 Q = fadd(ln.W[k], fshr<8>(ln.W[k]));
+            Q = fadd(Q, fshr<16>(Q));                        // byte i: decoded bytes of positions >= i
+            Q = Q << 1;                                      // 2 staging bytes per position
             endk = fadd(endk, fandi<0xFFu>(Q));              // staging address after the dword's output
-            const u32 R = fadd(Q, fadd(ln.N01[k], ln.N01[k]));   // interior positions: one slot further back
+            const u32 R = fadd(Q, ln.N02[k]);                // interior positions: one slot further back
             auto put = [](u32 t, u32 key) {
                 if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
-                else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(t) = (uint16_t)key;
+                else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
             };
             put(sub_byte<0>(endk, R), xk_lo);
             put(sub_byte<1>(endk, R), xk_lo >> 16);
@@ -789,9 +808,10 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
     if (nfl) {   // move the partial chunk to staging chunk 1
         if (lane < 8u) {
-            u32* s32 = reinterpret_cast<u32*>(stage);
-            s32[8u + lane] = s32[8u * (nfl + 1u) + lane];
-            s32[8u * (nfl + 1u) + lane] = 0u;
+            auto* from = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u * (nfl + 1u) + 4u * lane));
+            auto* to = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane));
+            *to = *from;
+            *from = 0u;
         }
         wave_lds_sync();
     }
@@ -821,7 +841,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
             for (u32 j = 0; j < 16u; ++j) {
                 u32 v = tv;
                 if (q == 0u && j < rel) {
-                    const u32 h = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(c1 + 2u * j);
+                    const u32 h = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(sswz(c1 + 2u * j));
                     cur = (h & kKeyFlag) ? (h & 0xFFu) : cur;
                     v = cur;
                 }
