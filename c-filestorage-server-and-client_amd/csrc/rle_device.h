@@ -863,6 +863,12 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
     vm_drain();
 }
 
+// Status of a stream the tiled path decoded (U = the buffer's decoded size): info bits for the two
+// properties encoder output never has, an unbounded final count and a decode short of U.
+__device__ __forceinline__ u32 dec_tiled_status(const DecState& st, u32 U) {
+    return st.tail ? RLE_STATUS_OPEN_TAIL : (st.out_pos < U ? RLE_STATUS_SHORT : RLE_STATUS_OK);
+}
+
 // Exact serial decode (src/rleCompression.c:47-62 semantics, writes capped at cap) for the
 // streams the tiled path declines: counts outside '1'..'9', unbounded counts before the last
 // token, or streams that decode to more than U bytes.  One lane; the encoder never emits these.

@@ -13,14 +13,17 @@
 // usable GPU it reports the problem and aborts.
 #include <hip/hip_runtime.h>
 #include <pthread.h>
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
 #include <chrono>
+#include <vector>
 
 #include "rleCompression.h"
+#include "rle_fileops.h"
 #include "rle_mi355x.h"
 
 namespace {
@@ -34,7 +37,7 @@ std::atomic<int> g_warned_overflow{0};
 
 // Host-path accounting (rle_mi355x_dropin_stats): bytes moved and wall time per phase.
 struct Stats {
-    std::atomic<uint64_t> calls_compress{0}, calls_decompress{0};
+    std::atomic<uint64_t> calls_compress{0}, calls_decompress{0}, calls_append{0};
     std::atomic<uint64_t> bytes_in{0}, bytes_out{0};        // caller bytes in / returned bytes out
     std::atomic<uint64_t> bytes_h2d{0}, bytes_d2h{0};
     std::atomic<uint64_t> ns_stage_in{0}, ns_device{0}, ns_stage_out{0};
@@ -67,10 +70,17 @@ struct Ctx {
     uint8_t* h_out = nullptr; size_t h_out_cap = 0;   // pinned staging: device -> caller block
     uint8_t* d_in = nullptr;  size_t d_in_cap = 0;
     uint8_t* d_out = nullptr; size_t d_out_cap = 0;
-    uint64_t* d_meta = nullptr;                      // [in_off, in_len, out_off, out_len, out_cap, status]
+    uint64_t* d_meta = nullptr;                      // kMetaSlots u64: per-launch [in_off, in_len, out_off, ...]
     uint64_t* h_meta = nullptr;                      // pinned mirror
     uint8_t* d_ws = nullptr;  size_t d_ws_cap = 0;    // segmented-path workspace
+    uint8_t* d_mid = nullptr; size_t d_mid_cap = 0;   // RLEappend: decoded old content ‖ new bytes
+    uint8_t* h_bm = nullptr;  size_t h_bm_cap = 0;    // RLEdecompressN: per-file offsets/lengths/status
+    uint8_t* d_bm = nullptr;  size_t d_bm_cap = 0;
 };
+// h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
+//   decode [in_off, in_len, out_off, out_len, out_cap, status], encode [in_off, in_len, out_off,
+//   out_len, -, status], append (rle_append_prepare_device's 4 u64)
+constexpr size_t kMetaDec = 0, kMetaEnc = 8, kMetaApp = 16, kMetaSlots = 24;
 
 // A worker thread's context is released by its pthread-key destructor, which can still be running
 // when the process exits (a thread joined by its creator has not necessarily finished its TLS
@@ -97,10 +107,13 @@ void free_ctx(void* p) {
     (void)hipHostFree(c->h_in);
     (void)hipHostFree(c->h_out);
     (void)hipHostFree(c->h_meta);
+    (void)hipHostFree(c->h_bm);
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_ws);
+    (void)hipFree(c->d_mid);
+    (void)hipFree(c->d_bm);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
     pthread_mutex_unlock(&g_exit_lock);
@@ -130,8 +143,8 @@ Ctx* ctx() {
     c->dev = (g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev);
     check(hipSetDevice(c->dev), "hipSetDevice");
     check(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking), "hipStreamCreate");
-    check(hipMalloc(&c->d_meta, 8 * sizeof(uint64_t)), "hipMalloc(meta)");
-    check(hipHostMalloc(&c->h_meta, 8 * sizeof(uint64_t), hipHostMallocDefault), "hipHostMalloc(meta)");
+    check(hipMalloc(&c->d_meta, kMetaSlots * sizeof(uint64_t)), "hipMalloc(meta)");
+    check(hipHostMalloc(&c->h_meta, kMetaSlots * sizeof(uint64_t), hipHostMallocDefault), "hipHostMalloc(meta)");
     pthread_setspecific(g_key, c);
     return c;
 }
@@ -155,6 +168,85 @@ void grow_dev(uint8_t*& p, size_t& cap, size_t need) {
 
 }  // namespace
 
+namespace {
+
+// Queues on c->s the encode of n device bytes at d_src (16-byte aligned) into c->d_out, the D2H of
+// C into h_meta[kMetaEnc + 3] and, up to kOneTripBytes, of the worst-case output into h_out (one
+// stream sync per call).  Returns whether the output travels with its size.
+bool queue_encode(Ctx* c, const uint8_t* d_src, size_t n) {
+    const size_t maxC = rle_max_compressed_size(n);
+    grow_dev(c->d_out, c->d_out_cap, round16(maxC));
+    uint64_t* hm = c->h_meta + kMetaEnc;
+    uint64_t* dm = c->d_meta + kMetaEnc;
+    hm[0] = 0; hm[1] = n; hm[2] = 0; hm[3] = 0;
+    check(hipMemcpyAsync(dm, hm, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
+    uint32_t* d_status = reinterpret_cast<uint32_t*>(dm + 5);
+    if (n >= kSegEncodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, n));
+    const int erc = n >= kSegEncodeBytes
+                        ? rle_encode_batch_device_seg(d_src, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, d_status, 1, n,
+                                                      c->d_ws, c->d_ws_cap, c->s)
+                        : rle_encode_batch_device(d_src, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, d_status, 1, c->s);
+    if (erc != RLE_OK) die("encode launch", hipGetLastError());
+    check(hipMemcpyAsync(hm + 3, dm + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
+    const bool one_trip = n <= kOneTripBytes;
+    if (one_trip) {
+        grow_host(c->h_out, c->h_out_cap, maxC);
+        check(hipMemcpyAsync(c->h_out, c->d_out, maxC, hipMemcpyDeviceToHost, c->s), "D2H");
+    }
+    return one_trip;
+}
+
+// After the stream sync that follows queue_encode: makes encoded bytes [from, C) present in h_out
+// and returns C.
+size_t fetch_encoded(Ctx* c, bool one_trip, size_t from) {
+    const size_t C = c->h_meta[kMetaEnc + 3];
+    if (!one_trip && C > from) {
+        grow_host(c->h_out, c->h_out_cap, C);
+        check(hipMemcpyAsync(c->h_out + from, c->d_out + from, C - from, hipMemcpyDeviceToHost, c->s), "D2H");
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    }
+    return C;
+}
+
+// The caller's block: head[0, headLen) ‖ h_out[from, C) ‖ 16 zero bytes (the reference's calloc'd
+// block ends in zeros that decoders read past C).  NULL on allocation failure; *outC always set.
+char* make_block(const Ctx* c, const char* head, size_t headLen, size_t from, size_t C, size_t* outC) {
+    const size_t total = headLen + (C - from);
+    *outC = total;
+    char* r = static_cast<char*>(malloc(total + 16));
+    if (!r) return nullptr;
+    if (headLen) memcpy(r, head, headLen);
+    memcpy(r + headLen, c->h_out + from, C - from);
+    memset(r + total, 0, 16);
+    return r;
+}
+
+// Queues the decode of C device bytes at d_src into d_dst (U decoded bytes, slot of cap bytes) and
+// the D2H of its status into h_meta[kMetaDec + 5].
+void queue_decode(Ctx* c, const uint8_t* d_src, size_t C, uint8_t* d_dst, size_t U, size_t cap) {
+    uint64_t* hm = c->h_meta + kMetaDec;
+    uint64_t* dm = c->d_meta + kMetaDec;
+    hm[0] = 0; hm[1] = C; hm[2] = 0; hm[3] = U; hm[4] = cap; hm[5] = 0;
+    check(hipMemcpyAsync(dm, hm, 6 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
+    uint32_t* d_status = reinterpret_cast<uint32_t*>(dm + 5);
+    if (C >= kSegDecodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, C));
+    const int drc = C >= kSegDecodeBytes
+                        ? rle_decode_batch_device_seg(d_src, dm + 0, dm + 1, d_dst, dm + 2, dm + 3, dm + 4, d_status, 1,
+                                                      C, c->d_ws, c->d_ws_cap, c->s)
+                        : rle_decode_batch_device(d_src, dm + 0, dm + 1, d_dst, dm + 2, dm + 3, dm + 4, d_status, 1,
+                                                  c->s);
+    if (drc != RLE_OK) die("decode launch", hipGetLastError());
+    check(hipMemcpyAsync(hm + 5, dm + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
+}
+
+void warn_overflow(const char* who) {
+    if (!g_warned_overflow.exchange(1))
+        fprintf(stderr, "librle_mi355x: %s: stream decodes past U+E (the reference would overflow its heap block); "
+                        "output truncated\n", who);
+}
+
+}  // namespace
+
 // src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes.
 extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize) {
     const size_t U = origSize;
@@ -163,52 +255,23 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
         return static_cast<char*>(calloc(16, 1));
     }
     Ctx* c = ctx();
-    const size_t maxC = rle_max_compressed_size(U);
     grow_host(c->h_in, c->h_in_cap, U);
     grow_dev(c->d_in, c->d_in_cap, round16(U));
-    grow_dev(c->d_out, c->d_out_cap, round16(maxC));
     const uint64_t t0 = now_ns();
     memcpy(c->h_in, data, U);
     const uint64_t t1 = now_ns();
-    c->h_meta[0] = 0; c->h_meta[1] = U; c->h_meta[2] = 0; c->h_meta[3] = 0;
     check(hipMemcpyAsync(c->d_in, c->h_in, U, hipMemcpyHostToDevice, c->s), "H2D");
-    check(hipMemcpyAsync(c->d_meta, c->h_meta, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
-    uint32_t* d_status = reinterpret_cast<uint32_t*>(c->d_meta + 5);
-    if (U >= kSegEncodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, U));
-    const int erc = U >= kSegEncodeBytes
-                        ? rle_encode_batch_device_seg(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
-                                                      c->d_meta + 3, d_status, 1, U, c->d_ws, c->d_ws_cap, c->s)
-                        : rle_encode_batch_device(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
-                                                  c->d_meta + 3, d_status, 1, c->s);
-    if (erc != RLE_OK) die("encode launch", hipGetLastError());
-    check(hipMemcpyAsync(c->h_meta + 3, c->d_meta + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
-    const bool one_trip = U <= kOneTripBytes;
-    if (one_trip) {
-        grow_host(c->h_out, c->h_out_cap, maxC);
-        check(hipMemcpyAsync(c->h_out, c->d_out, maxC, hipMemcpyDeviceToHost, c->s), "D2H");
-    }
+    const bool one_trip = queue_encode(c, c->d_in, U);
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-    const size_t C = c->h_meta[3];
-    if (!one_trip) {
-        grow_host(c->h_out, c->h_out_cap, C);
-        check(hipMemcpyAsync(c->h_out, c->d_out, C, hipMemcpyDeviceToHost, c->s), "D2H");
-        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-    }
+    const size_t C = fetch_encoded(c, one_trip, 0);
     const uint64_t t2 = now_ns();
-    char* r = static_cast<char*>(malloc(C + 16));
-    if (!r) {
-        *compressedSize = C;
-        return nullptr;
-    }
-    memcpy(r, c->h_out, C);
-    memset(r + C, 0, 16);
-    *compressedSize = C;
+    char* r = make_block(c, nullptr, 0, 0, C, compressedSize);
     const uint64_t t3 = now_ns();
     g_stats.calls_compress++;
     g_stats.bytes_in += U;
     g_stats.bytes_out += C;
     g_stats.bytes_h2d += U;
-    g_stats.bytes_d2h += one_trip ? maxC : C;
+    g_stats.bytes_d2h += one_trip ? rle_max_compressed_size(U) : C;
     g_stats.ns_stage_in += t1 - t0;
     g_stats.ns_device += t2 - t1;
     g_stats.ns_stage_out += t3 - t2;
@@ -232,22 +295,11 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     const uint64_t t0 = now_ns();
     memcpy(c->h_in, data, C);
     const uint64_t t1 = now_ns();
-    c->h_meta[0] = 0; c->h_meta[1] = C; c->h_meta[2] = 0; c->h_meta[3] = U; c->h_meta[4] = total; c->h_meta[5] = 0;
     check(hipMemcpyAsync(c->d_in, c->h_in, C, hipMemcpyHostToDevice, c->s), "H2D");
-    check(hipMemcpyAsync(c->d_meta, c->h_meta, 6 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s), "H2D(meta)");
-    uint32_t* d_status = reinterpret_cast<uint32_t*>(c->d_meta + 5);
-    if (C >= kSegDecodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, C));
-    const int drc = C >= kSegDecodeBytes
-                        ? rle_decode_batch_device_seg(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
-                                                      c->d_meta + 3, c->d_meta + 4, d_status, 1, C, c->d_ws,
-                                                      c->d_ws_cap, c->s)
-                        : rle_decode_batch_device(c->d_in, c->d_meta + 0, c->d_meta + 1, c->d_out, c->d_meta + 2,
-                                                  c->d_meta + 3, c->d_meta + 4, d_status, 1, c->s);
-    if (drc != RLE_OK) die("decode launch", hipGetLastError());
-    check(hipMemcpyAsync(c->h_meta + 5, c->d_meta + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
+    queue_decode(c, c->d_in, C, c->d_out, U, total);
     if (U) check(hipMemcpyAsync(c->h_out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-    const uint32_t st = (uint32_t)c->h_meta[5];
+    const uint32_t st = (uint32_t)c->h_meta[kMetaDec + 5];
     const uint64_t t2 = now_ns();
     memcpy(r, c->h_out, U);
     if (E) {
@@ -259,9 +311,7 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
             memset(r + U, 0, E);
         }
     }
-    if ((st & RLE_STATUS_OVERFLOW) && !g_warned_overflow.exchange(1))
-        fprintf(stderr, "librle_mi355x: RLEdecompress: stream decodes past U+E (the reference would overflow its "
-                        "heap block); output truncated\n");
+    if (st & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompress");
     const uint64_t t3 = now_ns();
     g_stats.calls_decompress++;
     g_stats.bytes_in += C;
@@ -274,10 +324,175 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     return r;
 }
 
+// src/filesystemApi.c:766-775 (decode, append, re-encode) fused into one device
+// round trip whose re-encode covers only c^r ‖ newContent (include/rle_fileops.h).
+extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompressedSize, const char* newContent,
+                           size_t newContentLen, size_t* newCompressedSize) {
+    const size_t C = contentSize, U = uncompressedSize, A = newContentLen;
+    // U == 0: the decode keeps nothing below U and whatever it writes into the extra region is
+    // overwritten by the appended bytes (:767-770), so the result is encode(newContent)
+    if (U == 0) return RLEcompress(const_cast<char*>(newContent), A, newCompressedSize);
+    Ctx* c = ctx();
+    const size_t offA = round16(C) + 16;   // d_in: old stream | splice head (16 B) | new bytes
+    const size_t inBytes = offA + A;
+    grow_host(c->h_in, c->h_in_cap, inBytes);
+    grow_dev(c->d_in, c->d_in_cap, round16(inBytes));
+    grow_dev(c->d_mid, c->d_mid_cap, round16(U + A));
+    const uint64_t t0 = now_ns();
+    if (C) memcpy(c->h_in, content, C);
+    if (A) memcpy(c->h_in + offA, newContent, A);
+    const uint64_t t1 = now_ns();
+    if (C) check(hipMemcpyAsync(c->d_in, c->h_in, C, hipMemcpyHostToDevice, c->s), "H2D");
+    if (A) check(hipMemcpyAsync(c->d_in + offA, c->h_in + offA, A, hipMemcpyHostToDevice, c->s), "H2D");
+    bool full = C == 0;   // no stream: the decoded content is U zero bytes (:48), re-encoded whole
+    bool one_trip = false;
+    if (full) {
+        check(hipMemsetAsync(c->d_mid, 0, U, c->s), "hipMemsetAsync");
+    } else {
+        queue_decode(c, c->d_in, C, c->d_mid, U, U);
+        if (rle_append_prepare_device(c->d_mid, U, c->d_in + offA - 16, c->d_meta + kMetaApp, c->s) != RLE_OK)
+            die("append launch", hipGetLastError());
+        check(hipMemcpyAsync(c->h_meta + kMetaApp, c->d_meta + kMetaApp, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                             c->s), "D2H(meta)");
+        one_trip = queue_encode(c, c->d_in + offA - 16, 16 + A);
+    }
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    size_t r = 0, tok = 0;
+    if (!full) {
+        // keep content[0, C - tok) only if the stream's final token is the one the encoder emits
+        // for the decoded tail c^r (and the decode saw encoder output)
+        const uint32_t st = (uint32_t)c->h_meta[kMetaDec + 5];
+        r = c->h_meta[kMetaApp + 1];
+        const uint8_t ch = reinterpret_cast<const uint8_t*>(c->h_meta + kMetaApp + 2)[15];
+        const uint8_t* y = reinterpret_cast<const uint8_t*>(content);
+        tok = r == 1 ? 1 : 3;
+        bool ok = st == RLE_STATUS_OK && r >= 1 && r <= 9 && C >= tok && y[C - tok] == ch;
+        if (ok && tok == 3) ok = y[C - 2] == ch && y[C - 1] == (uint8_t)('0' + r);
+        full = !ok;
+    }
+    char* out;
+    size_t Cn;
+    if (full) {
+        if (A) check(hipMemcpyAsync(c->d_mid + U, c->d_in + offA, A, hipMemcpyDeviceToDevice, c->s), "D2D");
+        one_trip = queue_encode(c, c->d_mid, U + A);
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        Cn = fetch_encoded(c, one_trip, 0);
+        out = make_block(c, nullptr, 0, 0, Cn, newCompressedSize);
+    } else {
+        const size_t skip = 16 - r;   // the filler's single-byte tokens
+        Cn = fetch_encoded(c, one_trip, skip);
+        out = make_block(c, content, C - tok, skip, Cn, newCompressedSize);
+    }
+    const uint64_t t2 = now_ns();
+    g_stats.calls_append++;
+    g_stats.bytes_in += C + A;
+    g_stats.bytes_out += *newCompressedSize;
+    g_stats.bytes_h2d += C + A;
+    g_stats.bytes_d2h += full ? Cn : Cn - (16 - r);
+    g_stats.ns_stage_in += t1 - t0;
+    g_stats.ns_device += t2 - t1;
+    return out;
+}
+
+// readNFilesHandler's decode loop (src/filesystemApi.c:675-687) and the
+// eviction loop (src/server.c:314-323) as one batched launch (include/rle_fileops.h).
+extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compressedSize,
+                              const size_t* uncompressedSize, char* const* out) {
+    if (n == 0) return 0;
+    if (!data || !compressedSize || !uncompressedSize || !out) {
+        errno = EINVAL;
+        return -1;
+    }
+    std::vector<size_t> idx;
+    size_t inTot = 0, outTot = 0, maxC = 0;
+    try {
+        idx.reserve(n);
+    } catch (...) {
+        errno = ENOMEM;
+        return -1;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        const size_t C = compressedSize[i], U = uncompressedSize[i];
+        if (C == 0) {  // calloc'd block (src/rleCompression.c:48)
+            if (U) memset(out[i], 0, U);
+            continue;
+        }
+        if (!data[i] || (U && !out[i])) {
+            errno = EINVAL;
+            return -1;
+        }
+        idx.push_back(i);
+        inTot += round16(C);
+        outTot += round16(U);
+        maxC = C > maxC ? C : maxC;
+    }
+    const size_t m = idx.size();
+    if (m == 0) return 0;
+    if (m > (1u << 30)) {
+        errno = EINVAL;
+        return -1;
+    }
+    Ctx* c = ctx();
+    // per-file metadata, one pinned block: in_off, in_len, out_off, out_len (m u64 each), status (m u32)
+    const size_t metaBytes = 32 * m + 4 * m;
+    grow_host(c->h_bm, c->h_bm_cap, metaBytes);
+    grow_dev(c->d_bm, c->d_bm_cap, round16(metaBytes));
+    grow_host(c->h_in, c->h_in_cap, inTot);
+    grow_host(c->h_out, c->h_out_cap, outTot);
+    grow_dev(c->d_in, c->d_in_cap, inTot);
+    grow_dev(c->d_out, c->d_out_cap, outTot);
+    const uint64_t t0 = now_ns();
+    uint64_t* hb = reinterpret_cast<uint64_t*>(c->h_bm);
+    size_t io = 0, oo = 0;
+    for (size_t k = 0; k < m; ++k) {
+        const size_t i = idx[k], C = compressedSize[i], U = uncompressedSize[i];
+        hb[k] = io; hb[m + k] = C; hb[2 * m + k] = oo; hb[3 * m + k] = U;
+        memcpy(c->h_in + io, data[i], C);
+        io += round16(C);
+        oo += round16(U);
+    }
+    const uint64_t t1 = now_ns();
+    uint64_t* db = reinterpret_cast<uint64_t*>(c->d_bm);
+    uint32_t* d_status = reinterpret_cast<uint32_t*>(db + 4 * m);
+    check(hipMemcpyAsync(c->d_in, c->h_in, inTot, hipMemcpyHostToDevice, c->s), "H2D");
+    check(hipMemcpyAsync(db, hb, 32 * m, hipMemcpyHostToDevice, c->s), "H2D(meta)");
+    if (maxC >= kSegDecodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes((uint32_t)m, inTot));
+    const int drc = maxC >= kSegDecodeBytes
+                        ? rle_decode_batch_device_seg(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr,
+                                                      d_status, (uint32_t)m, inTot, c->d_ws, c->d_ws_cap, c->s)
+                        : rle_decode_batch_device(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr,
+                                                  d_status, (uint32_t)m, c->s);
+    if (drc != RLE_OK) die("decode launch", hipGetLastError());
+    check(hipMemcpyAsync(c->h_out, c->d_out, outTot, hipMemcpyDeviceToHost, c->s), "D2H");
+    check(hipMemcpyAsync(hb + 4 * m, d_status, 4 * m, hipMemcpyDeviceToHost, c->s), "D2H(status)");
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const uint64_t t2 = now_ns();
+    const uint32_t* hst = reinterpret_cast<const uint32_t*>(hb + 4 * m);
+    size_t cin = 0, uout = 0;
+    for (size_t k = 0; k < m; ++k) {
+        const size_t i = idx[k], U = uncompressedSize[i];
+        if (U) memcpy(out[i], c->h_out + hb[2 * m + k], U);
+        if (hst[k] & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompressN");
+        cin += compressedSize[i];
+        uout += U;
+    }
+    const uint64_t t3 = now_ns();
+    g_stats.calls_decompress += m;
+    g_stats.bytes_in += cin;
+    g_stats.bytes_out += uout;
+    g_stats.bytes_h2d += inTot;
+    g_stats.bytes_d2h += outTot;
+    g_stats.ns_stage_in += t1 - t0;
+    g_stats.ns_device += t2 - t1;
+    g_stats.ns_stage_out += t3 - t2;
+    return 0;
+}
+
 extern "C" int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset) {
     if (!out) return RLE_E_INVAL;
     out->calls_compress = g_stats.calls_compress.load();
     out->calls_decompress = g_stats.calls_decompress.load();
+    out->calls_append = g_stats.calls_append.load();
     out->bytes_in = g_stats.bytes_in.load();
     out->bytes_out = g_stats.bytes_out.load();
     out->bytes_h2d = g_stats.bytes_h2d.load();
@@ -286,7 +501,7 @@ extern "C" int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset) {
     out->ns_device = g_stats.ns_device.load();
     out->ns_stage_out = g_stats.ns_stage_out.load();
     if (reset) {
-        g_stats.calls_compress = 0; g_stats.calls_decompress = 0; g_stats.bytes_in = 0; g_stats.bytes_out = 0;
+        g_stats.calls_compress = 0; g_stats.calls_decompress = 0; g_stats.calls_append = 0; g_stats.bytes_in = 0; g_stats.bytes_out = 0;
         g_stats.bytes_h2d = 0; g_stats.bytes_d2h = 0; g_stats.ns_stage_in = 0; g_stats.ns_device = 0;
         g_stats.ns_stage_out = 0;
     }
@@ -305,10 +520,11 @@ struct StatsAtExit {
         FILE* f = fopen(path, "w");
         if (!f) return;
         fprintf(f,
-                "{\"calls_compress\": %llu, \"calls_decompress\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, "
+                "{\"calls_compress\": %llu, \"calls_decompress\": %llu, \"calls_append\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, "
                 "\"bytes_h2d\": %llu, \"bytes_d2h\": %llu, \"ns_stage_in\": %llu, \"ns_device\": %llu, "
                 "\"ns_stage_out\": %llu}\n",
                 (unsigned long long)s.calls_compress, (unsigned long long)s.calls_decompress,
+                (unsigned long long)s.calls_append,
                 (unsigned long long)s.bytes_in, (unsigned long long)s.bytes_out, (unsigned long long)s.bytes_h2d,
                 (unsigned long long)s.bytes_d2h, (unsigned long long)s.ns_stage_in, (unsigned long long)s.ns_device,
                 (unsigned long long)s.ns_stage_out);

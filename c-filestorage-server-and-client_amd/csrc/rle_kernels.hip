@@ -140,7 +140,10 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
         if (st.serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
-        else dec_finish(st, U, lane, stage, rso, dst);
+        else {
+            dec_finish(st, U, lane, stage, rso, dst);
+            stat = dec_tiled_status(st, U);
+        }
         RLE_STAMP(st.sp, 7);   // finish
 #if RLE_STAMPS
         if (lane == 0) {

@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         });
         const bool last = g + 1u == s0 + nseg;
         dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
-        if (last && lane == 0 && status) status[b] = st.serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : RLE_STATUS_OK;
+        if (last && lane == 0 && status) status[b] = st.serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : dec_tiled_status(st, U);
     }
 }
 

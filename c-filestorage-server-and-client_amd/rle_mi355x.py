@@ -23,6 +23,8 @@ RLE_STATUS_OK = 0
 RLE_STATUS_OVERFLOW = 1
 RLE_STATUS_MISALIGNED = 2
 RLE_STATUS_SERIAL = 0x100
+RLE_STATUS_OPEN_TAIL = 0x200
+RLE_STATUS_SHORT = 0x400
 
 _u64p = ctypes.c_void_p
 _lib = None
@@ -37,7 +39,7 @@ class RLEError(RuntimeError):
 class DropinStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("calls_compress", "calls_decompress", "bytes_in", "bytes_out",
                                                "bytes_h2d", "bytes_d2h", "ns_stage_in", "ns_device",
-                                               "ns_stage_out")]
+                                               "ns_stage_out", "calls_append")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -78,6 +80,12 @@ def lib():
     L.RLEcompress.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.RLEdecompress.restype = ctypes.c_void_p
     L.RLEdecompress.argtypes = [ctypes.c_char_p, sz, sz, sz]
+    L.RLEappend.restype = ctypes.c_void_p
+    L.RLEappend.argtypes = [ctypes.c_char_p, sz, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.RLEdecompressN.restype = ctypes.c_int
+    L.RLEdecompressN.argtypes = [sz, vp, vp, vp, vp]
+    L.rle_append_prepare_device.restype = ctypes.c_int
+    L.rle_append_prepare_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp]
     _lib = L
     return L
 
@@ -110,6 +118,36 @@ def decompress(stream: bytes, U: int, E: int = 0) -> bytes:
     out = ctypes.string_at(p, U + E) if U + E else b""
     _libc.free(p)
     return out
+
+
+def append(content: bytes, U: int, new: bytes) -> bytes:
+    """RLEappend (include/rle_fileops.h): the write path of src/filesystemApi.c:766-775
+    -- decode(content, U) ‖ new, re-encoded -- as one fused device round trip."""
+    c = ctypes.c_size_t(0)
+    p = lib().RLEappend(content, len(content), U, new, len(new), ctypes.byref(c))
+    if not p:
+        raise MemoryError("RLEappend returned NULL")
+    out = ctypes.string_at(p, c.value) if c.value else b""
+    _libc.free(p)
+    return out
+
+
+def decompress_n(streams, usizes):
+    """RLEdecompressN (include/rle_fileops.h): the n decodes of readNFiles
+    (src/filesystemApi.c:675-687) / eviction (src/server.c:314-323) in one launch, into caller buffers."""
+    n = len(streams)
+    if n != len(usizes):
+        raise ValueError("streams and usizes differ in length")
+    keep = [ctypes.create_string_buffer(s, len(s) + 1) for s in streams]
+    outs = [ctypes.create_string_buffer(max(int(u), 1)) for u in usizes]
+    data = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in keep])
+    cs = (ctypes.c_size_t * max(n, 1))(*[len(s) for s in streams])
+    us = (ctypes.c_size_t * max(n, 1))(*[int(u) for u in usizes])
+    op = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in outs])
+    rc = lib().RLEdecompressN(n, data, cs, us, op)
+    if rc != 0:
+        raise RLEError(f"RLEdecompressN failed (errno {ctypes.get_errno()})")
+    return [o.raw[:int(u)] for o, u in zip(outs, usizes)]
 
 
 # ------------------------------------------------------------------ batch layout helpers

@@ -45,6 +45,10 @@ extern "C" {
 #define RLE_STATUS_MISALIGNED  2u      /* input or output slot not 16-byte aligned; buffer skipped */
 #define RLE_STATUS_TOOLARGE    4u      /* buffer larger than 0x7FFFFFF0 bytes (2 GiB); buffer skipped */
 #define RLE_STATUS_SERIAL      0x100u  /* info: stream decoded by the exact serial path (not encoder output) */
+#define RLE_STATUS_OPEN_TAIL   0x200u  /* info: the final token's count digit lies past C and reads as the zero
+                                          padding, so its byte fills up to U (not encoder output) */
+#define RLE_STATUS_SHORT       0x400u  /* info: the stream decodes to fewer than U bytes, the rest is zero
+                                          (not encoder output) */
 
 /* Worst-case compressed size of U bytes (every run of length 2: 3 bytes per 2 input bytes). */
 size_t rle_max_compressed_size(size_t U);
@@ -75,6 +79,7 @@ typedef struct {
     uint64_t calls_compress, calls_decompress;
     uint64_t bytes_in, bytes_out, bytes_h2d, bytes_d2h;
     uint64_t ns_stage_in, ns_device, ns_stage_out;
+    uint64_t calls_append;   /* RLEappend (include/rle_fileops.h); RLEdecompressN counts per file */
 } rle_dropin_stats_t;
 int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
 
@@ -103,6 +108,16 @@ int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_in_off, cons
                                 const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
                                 uint64_t total_in_bytes, void* d_workspace, size_t workspace_bytes,
                                 void* stream);
+
+/* Fused append, device half (used by RLEappend, include/rle_fileops.h).
+ * d_mid holds the decoded old content, U >= 1 bytes, 16-byte aligned.  Finds the final run of
+ * d_mid (byte c, length L), r = (L - 1) % 9 + 1 (the size of the reference encoder's last token of
+ * that run, src/rleCompression.c:22-39), and writes the 16-byte splice head
+ *   d_head[0, 16) = (16 - r) filler bytes ‖ c^r
+ * whose filler encodes to itself byte for byte, so encode(head ‖ new) = filler ‖ encode(c^r ‖ new).
+ * d_meta (4 u64, device): [0] final run start, [1] r, [2..3] a copy of the head.  Asynchronous on
+ * `stream`; RLE_E_INVAL when U == 0. */
+int rle_append_prepare_device(const void* d_mid, uint64_t U, void* d_head, uint64_t* d_meta, void* stream);
 
 /* Diagnostic builds only (RLE_STAMPS=1, never the product library): per-segment decode cycle sums
  * over all waves: [tile wait, scan, scatter, flush reads, flush fill, flush store, flush re-zero,

@@ -31,7 +31,8 @@ def declared_functions():
 def test_library_exports_every_declared_symbol():
     L = R.lib()
     names = declared_functions()
-    assert {"RLEcompress", "RLEdecompress", "rle_encode_batch_device", "rle_decode_batch_device"} <= names
+    assert {"RLEcompress", "RLEdecompress", "rle_encode_batch_device", "rle_decode_batch_device", "RLEappend",
+            "RLEdecompressN", "rle_append_prepare_device"} <= names
     for n in sorted(names):
         assert hasattr(L, n), f"librle_mi355x.so does not export {n}"
 
@@ -53,9 +54,12 @@ def test_reference_prototypes_exact():
 
 
 def test_headers_compile_as_c99():
-    code = '#include "rleCompression.h"\n#include "rle_mi355x.h"\nint main(void){size_t c=0;(void)c;' \
+    code = '#include "rleCompression.h"\n#include "rle_mi355x.h"\n#include "rle_fileops.h"\n' \
+           'int main(void){size_t c=0;(void)c;' \
            'char*(*f)(char*,size_t,size_t*)=RLEcompress;char*(*g)(char*,size_t,size_t,size_t)=RLEdecompress;' \
-           '(void)f;(void)g;return 0;}\n'
+           'char*(*a)(char*,size_t,size_t,const char*,size_t,size_t*)=RLEappend;' \
+           'int(*n)(size_t,char*const*,const size_t*,const size_t*,char*const*)=RLEdecompressN;' \
+           '(void)f;(void)g;(void)a;(void)n;return 0;}\n'
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "t.c")
         open(p, "w").write(code)

@@ -1,0 +1,111 @@
+"""GPU parity of the fused / batched file operations (include/rle_fileops.h, SURVEY.md §8 (f1),
+(f2), (f4)) against the reference composition they replace, restated with the oracle:
+
+  append   src/filesystemApi.c:766-775   decode(content, U, E=len(new)) ; memcpy at U ; encode(U+len(new))
+  readN    src/filesystemApi.c:675-687   RLEdecompress(content_i, C_i, U_i, 0) per file
+  evict    src/server.c:314-323          the same decode per victim
+
+Bit-exact everywhere."""
+import numpy as np
+import pytest
+
+import rle_mi355x as R
+import rle_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_append(content, U, new):
+    """src/filesystemApi.c:767-774 with the oracle in place of src/rleCompression.c."""
+    d, _ = O.decode(content, U, U + len(new))
+    return O.encode(d[:U] + new)
+
+
+def _runs(rng, n, alpha, maxrun):
+    vals = rng.choice(np.frombuffer(alpha, np.uint8), size=n)
+    reps = rng.integers(1, maxrun + 1, size=n)
+    return np.repeat(vals, reps).tobytes()
+
+
+def test_append_final_run_remainders():
+    # old content ending in a run of every length 1..40 (all remainders r = 1..9, several 9-tokens),
+    # appended bytes that continue the run, break it, or are empty
+    cases = []
+    for ch in (b"a", b"9", b"1", b"\0", b"\xff"):
+        for L in range(1, 41):
+            old = b"xy" + ch * L
+            for new in (b"", ch, ch * 8, ch * 9, ch * 20 + b"z", b"z", b"zz" + ch, bytes(range(50))):
+                cases.append((old, new))
+    for old, new in cases:
+        y = O.encode(old)
+        assert R.append(y, len(old), new) == ref_append(y, len(old), new), (old, new)
+
+
+def test_append_digit_heavy_streams():
+    # streams whose bytes are digits, where the final token cannot be found by reading backwards
+    rng = np.random.default_rng(11)
+    for i in range(400):
+        old = _runs(rng, int(rng.integers(1, 60)), b"23456789" if i % 2 else b"99a1", 12)
+        new = _runs(rng, int(rng.integers(0, 30)), b"2399", 12)
+        y = O.encode(old)
+        assert R.append(y, len(old), new) == O.encode(old + new), (old, new)
+
+
+def test_append_chained_writes_build_the_file():
+    # a file written by successive appends, as the server does (a new file starts empty, :351)
+    rng = np.random.default_rng(5)
+    for kind in range(5):
+        content, plain = b"", b""
+        for k in range(30):
+            n = int(rng.integers(0, 3000))
+            new = O.gen(kind, 100 * kind + k, n)
+            content = R.append(content, len(plain), new)
+            plain += new
+            assert content == O.encode(plain), (kind, k)
+
+
+def test_append_large_and_segmented_sizes():
+    for old, new in [(bytes(1 << 20), bytes(5000)), (O.gen(1, 1, 300000), O.gen(2, 2, 200000)),
+                     (O.gen(3, 3, 70000), b""), (b"q" * 100001, b"q" * 7), (O.gen(2, 4, 5), O.gen(1, 5, 1 << 20))]:
+        y = O.encode(old)
+        assert R.append(y, len(old), new) == O.encode(old + new), (len(old), len(new))
+
+
+def test_append_empty_and_not_encoder_streams():
+    assert R.append(b"", 0, b"") == b""
+    assert R.append(b"", 0, b"aaab") == b"aa3b"
+    # no stream but U > 0: the reference decodes U zero bytes (src/rleCompression.c:48)
+    assert R.append(b"", 5, b"ab") == ref_append(b"", 5, b"ab")
+    # hand-made streams the encoder never emits: non-canonical final token, bad digits, a stream
+    # that decodes past U or short of it -- all re-encoded whole, as the reference does
+    for content, U, new in [(b"aa2aa2", 4, b"ab"), (b"aa1", 1, b"a"), (b"aaz", 1, b"q"), (b"aa9", 3, b"a"),
+                            (b"abc", 5, b"cc"), (b"a", 3, b"\0"), (b"xx5yy7", 12, b"y"), (b"11", 1, b"1")]:
+        assert R.append(content, U, new) == ref_append(content, U, new), (content, U, new)
+
+
+def test_decompress_n_matches_per_file_decodes():
+    rng = np.random.default_rng(7)
+    xs = [O.gen(i % 5, i, int(rng.integers(0, 20000))) for i in range(300)]
+    xs += [b"", b"a", bytes(70000), O.gen(1, 9, 200000)]   # empty, tiny, and segmented-path sizes
+    ys = [O.encode(x) for x in xs]
+    got = R.decompress_n(ys, [len(x) for x in xs])
+    bad = [i for i in range(len(xs)) if got[i] != xs[i]]
+    assert not bad, bad[:5]
+
+
+def test_decompress_n_reference_semantics_on_odd_streams():
+    # C == 0 with U > 0 (zeros), U shorter than the stream, invalid digits: each equal to RLEdecompress
+    streams = [b"", b"aa9aa9", b"aaz", b"ab", b"xx5", b"\0\0\0"]
+    us = [7, 4, 3, 6, 5, 2]
+    got = R.decompress_n(streams, us)
+    for s, u, g in zip(streams, us, got):
+        assert g == O.decode(s, u)[0], (s, u)
+        assert g == R.decompress(s, u), (s, u)
+    assert R.decompress_n([], []) == []
+
+
+def test_decompress_n_readn_batch_of_fixture_files(dummyfiles):
+    from conftest import committed_file_bytes
+    xs = [x for x in (committed_file_bytes(e) for e in dummyfiles["files"]) if x is not None]
+    ys = [R.compress(x) for x in xs]
+    assert R.decompress_n(ys, [len(x) for x in xs]) == xs
