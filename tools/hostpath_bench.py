@@ -83,18 +83,102 @@ def threads(T, U, seconds):
     return {"threads": T, "U": U, "roundtrips": sum(counts), "roundtrip_GBps": sum(counts) * U / el / 1e9}
 
 
+def _timeit(fn, seconds):
+    fn()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        n += 1
+    return (time.perf_counter() - t0) / n
+
+
+def write_path(L, x, new):
+    """src/filesystemApi.c:767-775 through codec library L (decode with E extra, memcpy, encode)."""
+    y_c = ctypes.c_size_t(0)
+    U = len(x)
+
+    def run(y, C):
+        d = L.RLEdecompress(y, C, U, len(new))
+        ctypes.memmove(d + U, new, len(new))
+        p = L.RLEcompress(ctypes.cast(d, ctypes.c_char_p), U + len(new), ctypes.byref(y_c))
+        R._libc.free(d)
+        R._libc.free(p)
+    return run
+
+
+def fileops(seconds):
+    """SURVEY §8 (f1) fused append vs the reference's three-call write path, and (f2)/(f4) one
+    batched RLEdecompressN vs a loop of RLEdecompress calls (readNFiles / eviction)."""
+    L = R.lib()
+    L.RLEdecompress.restype = ctypes.c_void_p
+    out = {"append": [], "readN": []}
+    ref = None
+    try:
+        sys.path[:0] = [os.path.join(REPO, "oracle")]
+        import rle_oracle as O
+        ref = O.reference()   # the compiled reference codec (oracle/_ref), CPU, one thread
+    except Exception:
+        O = None
+    for kind, U, A in (("random", 4096, 4096), ("runs", 65536, 4096), ("random", 1 << 20, 4096),
+                       ("zero", 4 << 20, 65536), ("runs", 4 << 20, 65536)):
+        x, new = gen(kind, U, 3), gen(kind, A, 4)
+        y = R.compress(x)
+        C = len(y)
+        c = ctypes.c_size_t(0)
+
+        def fused():
+            p = L.RLEappend(y, C, U, new, A, ctypes.byref(c))
+            R._libc.free(p)
+        t_f = _timeit(fused, seconds)
+        t_c = _timeit(lambda: write_path(L, x, new)(y, C), seconds)
+        row = {"kind": kind, "U": U, "A": A, "C": C, "fused_us": t_f * 1e6, "composed_gpu_us": t_c * 1e6}
+        if ref is not None:
+            ypad = y + b"\0\0\0"
+            t_r = _timeit(lambda: write_path(ref, x, new)(ypad, C), min(seconds, 2.0))
+            row["reference_cpu_us"] = t_r * 1e6
+        out["append"].append(row)
+        print(f"append {kind} {U} done", file=sys.stderr, flush=True)
+    for n, U in ((64, 4096), (256, 4096), (64, 65536), (16, 1 << 20)):
+        xs = [gen(("random", "zero", "runs")[i % 3], U, i) for i in range(n)]
+        ys = [R.compress(x) for x in xs]
+        bufs = [ctypes.create_string_buffer(U) for _ in range(n)]
+        keep = [ctypes.create_string_buffer(y, len(y) + 3) for y in ys]
+        data = (ctypes.c_void_p * n)(*[ctypes.addressof(k) for k in keep])
+        cs = (ctypes.c_size_t * n)(*[len(y) for y in ys])
+        us = (ctypes.c_size_t * n)(*([U] * n))
+        op = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+
+        def batched():
+            assert L.RLEdecompressN(n, data, cs, us, op) == 0
+
+        def looped():
+            for k in range(n):
+                p = L.RLEdecompress(keep[k], cs[k], U, 0)
+                ctypes.memmove(bufs[k], p, U)
+                R._libc.free(p)
+        t_b = _timeit(batched, seconds)
+        t_l = _timeit(looped, seconds)
+        assert all(bufs[k].raw == xs[k] for k in range(n))
+        out["readN"].append({"files": n, "U": U, "batched_us": t_b * 1e6, "looped_us": t_l * 1e6,
+                             "batched_GBps": n * U / t_b / 1e9, "looped_GBps": n * U / t_l / 1e9})
+        print(f"readN {n}x{U} done", file=sys.stderr, flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=1.0)
-    ap.add_argument("--only", choices=["single", "threads"], default=None)
+    ap.add_argument("--only", choices=["single", "threads", "fileops"], default=None)
     a = ap.parse_args()
     R.dropin_stats(reset=True)
     res = {"single": [], "threads": []}
-    if a.only != "threads":
+    if a.only in (None, "single"):
         for U in (4096, 65536, 1 << 20, 4 << 20):
             for kind in ("random", "zero", "runs"):
                 res["single"].append(one(kind, U, a.seconds))
-    if a.only != "single":
+    if a.only in (None, "fileops"):
+        res["fileops"] = fileops(a.seconds)
+    if a.only in (None, "threads"):
         for T in (1, 4, 8):
             res["threads"].append(threads(T, 1 << 20, a.seconds))
             print(f"threads {T} done", file=sys.stderr, flush=True)
