@@ -191,29 +191,49 @@ struct Refill {
     u32x4 rs;
     u32 voff;   // lane byte offset of tile t+2
     u32 lds;    // slot LDS address
-    __device__ __forceinline__ void operator()() const { dma_tile(rs, voff, lds); }
+    bool on;    // tile t+2 exists (wave-uniform)
+    __device__ __forceinline__ void operator()() const {
+        if (on) dma_tile(rs, voff, lds);
+    }
 };
 // Tiles start at `start` (bytes from the buffer descriptor's base): tile t is [start + 1008 t, ...).
-template <class Step>
-__device__ __forceinline__ void walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots,
-                                           Step step) {
+// The first two tiles' loads; walk_tiles issues them itself unless the caller did (primed), e.g. to
+// overlap their latency with its own setup.
+__device__ __forceinline__ void walk_prime(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots) {
     const u32 lo = start + 16u * lane;
     const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
-    dma_tile(rs, lo, l0);
-    dma_tile(rs, kTileStep + lo, l1);
+    if (ntiles) dma_tile(rs, lo, l0);
+    if (ntiles > 1u) dma_tile(rs, kTileStep + lo, l1);
+}
+template <class Step>
+__device__ __forceinline__ void walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots,
+                                           Step step, bool primed = false) {
+    const u32 lo = start + 16u * lane;
+    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
+    // Only tiles that exist are loaded, so before step t the ops issued after tile t's load are
+    // step t-2's stores, tile t+1's load (if t+1 < ntiles) and step t-1's stores.  Stores are never
+    // waited for: nothing in the wave reads them back, and a wave may end with stores in flight.
+    // Loads are all consumed by the last step, so only a walk that stops early (~0u) drains.
+    if (!primed) walk_prime(rs, start, ntiles, lane, slots);
     u32 p1 = 0, p2 = 0;   // stores of the last step and of the one before
     for (u32 t = 0; t < ntiles; t += 2) {
-        vm_wait(p2 + 1u + p1);
+        vm_wait(p2 + (t + 1u < ntiles ? 1u : 0u) + p1);
         p2 = p1;
-        p1 = step(t, slots, Refill{rs, (t + 2u) * kTileStep + lo, l0});
-        if (p1 == ~0u || t + 1u >= ntiles) break;
-        vm_wait(p2 + 1u + p1);
+        p1 = step(t, slots, Refill{rs, (t + 2u) * kTileStep + lo, l0, t + 2u < ntiles});
+        if (p1 == ~0u) {
+            vm_drain();
+            return;
+        }
+        if (t + 1u >= ntiles) break;
+        vm_wait(p2 + (t + 2u < ntiles ? 1u : 0u) + p1);
         p2 = p1;
-        p1 = step(t + 1u, slots + kSlot, Refill{rs, (t + 3u) * kTileStep + lo, l1});
-        if (p1 == ~0u) break;
+        p1 = step(t + 1u, slots + kSlot, Refill{rs, (t + 3u) * kTileStep + lo, l1, t + 3u < ntiles});
+        if (p1 == ~0u) {
+            vm_drain();
+            return;
+        }
     }
-    vm_drain();
 }
 __device__ __forceinline__ u32 ntiles_for(u32 n) { return (n + kTileStep - 1u) / kTileStep; }
 
@@ -546,13 +566,22 @@ struct DecState {
     Stamps sp;     // diagnostic builds only
 };
 
-// Bank spread (RLE_SWZ): dword i of the staging chunk at byte address A (32-aligned) lives at
-// A + 4 (i ^ g), g = bits 7..9 of A.  A random-data tile decodes 16 positions (32 B) per lane and
-// a zero-fill tile 48 (96 B): unswizzled, each scatter write hits 4 of the 32 banks.
+// Bank spread of the decode staging (RLE_SWZ).  Unswizzled, a random-data tile decodes 16 positions
+// (32 B of keys) per lane, so the lanes of one scatter write sit 32 B apart and 8 of every 32-lane
+// group share a bank.  Mode 1: dword i of the 32-B chunk at A lives at A + 4 (i ^ g), g = bits 7..9
+// of A (flush reads dword by dword).  Mode 2: the 16-B slot s of the 128-B row at A lives at slot
+// s ^ g, g = bits 7..9 of A, so the lanes 128 B apart land in 8 different slots and the flush still
+// reads each 16-B half of a chunk with one ds_read_b128.  Every staging access goes through sswz;
+// the staging is 128-B aligned, so a row never leaves it.
 #ifndef RLE_SWZ
 #define RLE_SWZ 0
 #endif
-__device__ __forceinline__ u32 sswz(u32 t) { return RLE_SWZ ? bitop3<0xF0 ^ (0xCC & 0xAA)>(t, t >> 5, 0x1Cu) : t; }
+__device__ __forceinline__ u32 sswz(u32 t) {
+    if (RLE_SWZ == 1) return bitop3<0xF0 ^ (0xCC & 0xAA)>(t, t >> 5, 0x1Cu);
+    if (RLE_SWZ == 2) return bitop3<0xF0 ^ (0xCC & 0xAA)>(t, t >> 3, 0x70u);
+    return t;
+}
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
@@ -564,11 +593,14 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         u32x4* s4 = reinterpret_cast<u32x4*>(stage + 32u * (c + 1u));
         u32x4 a = u32x4{0u, 0u, 0u, 0u}, b = a;
         if (active) {
-            if (RLE_SWZ) {
+            if (RLE_SWZ == 1) {
                 const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
                 auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
                 a = u32x4{rd(0), rd(1), rd(2), rd(3)};
                 b = u32x4{rd(4), rd(5), rd(6), rd(7)};
+            } else if (RLE_SWZ == 2) {
+                a = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4)));
+                b = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4) + 16u));
             } else {
                 a = s4[0];
                 b = s4[1];
@@ -608,8 +640,13 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         head = 0;
         RLE_STAMP(sp, 5);   // flush: store issue
         if (active) {
-            s4[0] = u32x4{0u, 0u, 0u, 0u};
-            s4[1] = u32x4{0u, 0u, 0u, 0u};
+            if (RLE_SWZ == 2) {
+                *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(s4))) = u32x4{0u, 0u, 0u, 0u};
+                *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(s4) + 16u)) = u32x4{0u, 0u, 0u, 0u};
+            } else {
+                s4[0] = u32x4{0u, 0u, 0u, 0u};
+                s4[1] = u32x4{0u, 0u, 0u, 0u};
+            }
         }
         const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
         fillc = readlane(lastb, lastlane);
@@ -859,14 +896,17 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
         }
     }
     wave_lds_sync();
-    if (lane < 8u) reinterpret_cast<u32*>(stage)[8u + lane] = 0u;   // staging chunk 1 back to zero
-    vm_drain();
+    if (lane < 8u)   // staging chunk 1 back to zero
+        *reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane)) = 0u;
 }
 
-// Status of a stream the tiled path decoded (U = the buffer's decoded size): info bits for the two
-// properties encoder output never has, an unbounded final count and a decode short of U.
+// Status of a stream the tiled path decoded (U = the buffer's decoded size): the info bit SHORT when
+// its tokens decode to fewer than U bytes, which encoder output never does.  (An unbounded final
+// token reaches the tiled path only as a single 0x00 byte followed by the zero padding, where the
+// reference's fill to U writes the zeros its calloc'd block already holds: encoder output can end
+// that way, so it is not flagged.)
 __device__ __forceinline__ u32 dec_tiled_status(const DecState& st, u32 U) {
-    return st.tail ? RLE_STATUS_OPEN_TAIL : (st.out_pos < U ? RLE_STATUS_SHORT : RLE_STATUS_OK);
+    return st.out_pos < U ? RLE_STATUS_SHORT : RLE_STATUS_OK;
 }
 
 // Exact serial decode (src/rleCompression.c:47-62 semantics, writes capped at cap) for the

@@ -21,6 +21,10 @@ __device__ __forceinline__ u32 xcd_buffer(u32 wg, u32 ngrid, u32 waves, u32 wid)
 #endif
 }
 
+#ifndef RLE_NOWALK   // fixed-cost probe builds only (wrong output): no tiles walked
+#define RLE_NOWALK 0
+#endif
+
 #ifndef RLE_ENC_WAVES
 #define RLE_ENC_WAVES 4
 #endif
@@ -61,7 +65,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
     st.sp.last = memtime();
 #endif
-    walk_tiles(rsi, 0u, ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+    walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         return enc_tile(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st);
     });
     RLE_STAMP(st.sp, 6);   // drain
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ out_cap,
                                                            uint32_t* __restrict__ status, uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
-    __shared__ __attribute__((aligned(64))) uint8_t stage_all[kDecWaves * kDecStage];
+    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kDecStage];
     __shared__ DecEntry tbl[256];
 #ifdef RLE_LDS_PAD   // occupancy experiments only
     __shared__ uint8_t ldspad[RLE_LDS_PAD];
@@ -105,38 +109,53 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
 #endif
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
-    for (u32 k = threadIdx.x; k < 256u; k += kDecBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
+    // Setup order overlaps latencies: the buffer's metadata and the phase table are loaded
+    // together, and the first two tiles' DMA is issued before the staging is zeroed.  (The table
+    // is stored first: the compiler does not count the DMA loads, so a wait for the table after
+    // them would wait for them too.)
+    constexpr u32 kTblPer = (256u + kDecBlock - 1u) / kDecBlock;
+    DecEntry te[kTblPer];
+#pragma unroll
+    for (u32 i = 0; i < kTblPer; ++i) te[i] = dec_entry_from(kDecTable.e[(threadIdx.x + i * kDecBlock) & 255u]);
+    const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
+    // all five per-buffer words are loaded at once, unconditionally (index clamped; n >= 1)
+    const u32 bi = b < n ? b : 0u;
+    const uint64_t* capp = out_cap ? out_cap : out_len;
+    const uint64_t C64 = in_len[bi], U64 = out_len[bi], cap = capp[bi];
+    const uint8_t* src = in + in_off[bi];
+    uint8_t* dst = out + out_off[bi];
+    u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
+    if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+    const u32 C = (u32)C64, U = (u32)U64;
+    const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+    const u32 ntiles = (b < n && !bad && !RLE_NOWALK) ? ntiles_for(C) : 0u;
     uint8_t* stage = stage_all + wid * kDecStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
+#pragma unroll
+    for (u32 i = 0; i < kTblPer; ++i) tbl[(threadIdx.x + i * kDecBlock) & 255u] = te[i];
+    walk_prime(rsi, 0u, ntiles, lane, slots);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     if (kDecWaves > 1) __syncthreads();
     else wave_lds_sync();
 
-    const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
     if (b < n) {
-        const uint64_t C64 = in_len[b];
-        const uint64_t U64 = out_len[b];
-        const uint64_t cap = out_cap ? out_cap[b] : U64;
-        const uint8_t* src = in + in_off[b];
-        uint8_t* dst = out + out_off[b];
-        u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
-        if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
         if (bad) {
             if (lane == 0 && status) status[b] = bad;
             return;
         }
-        const u32 C = (u32)C64, U = (u32)U64;
-        const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
         DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, {}};
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
         st.sp.last = memtime();
 #endif
-        walk_tiles(rsi, 0u, ntiles_for(C), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st);
-        });
+        walk_tiles(
+            rsi, 0u, ntiles, lane, slots,
+            [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st);
+            },
+            true);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
         if (st.serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);

@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
                                                                   const uint2* __restrict__ plan,
                                                                   const u32* __restrict__ bflag) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
-    __shared__ __attribute__((aligned(64))) uint8_t stage_all[kSegWaves * kDecStage];
+    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kDecStage];
     __shared__ DecEntry tbl[256];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);

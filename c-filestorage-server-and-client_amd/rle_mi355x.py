@@ -23,7 +23,6 @@ RLE_STATUS_OK = 0
 RLE_STATUS_OVERFLOW = 1
 RLE_STATUS_MISALIGNED = 2
 RLE_STATUS_SERIAL = 0x100
-RLE_STATUS_OPEN_TAIL = 0x200
 RLE_STATUS_SHORT = 0x400
 
 _u64p = ctypes.c_void_p

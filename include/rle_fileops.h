@@ -15,8 +15,8 @@
  *    rle_mi355x.h rle_append_prepare_device), which equals the reference result whenever `content`
  *    is encoder output — the only content the server stores (filesystemApi.c:774 -> :812; a new
  *    file starts empty, :351).  Streams detected as not encoder output (invalid counts, output
- *    past U, a final token that disagrees with the decoded tail) are re-encoded whole, as the
- *    reference does; other hand-made streams keep their non-canonical prefix.
+ *    past U or short of it, a final token that disagrees with the decoded tail) are re-encoded
+ *    whole, as the reference does; other hand-made streams keep their non-canonical prefix.
  *
  *  - RLEdecompressN (f2, f4) decodes n stored files in one launch: readNFilesHandler's loop
  *    (src/filesystemApi.c:675-687) and the eviction loop (src/server.c:314-323).  File i is

@@ -45,8 +45,6 @@ extern "C" {
 #define RLE_STATUS_MISALIGNED  2u      /* input or output slot not 16-byte aligned; buffer skipped */
 #define RLE_STATUS_TOOLARGE    4u      /* buffer larger than 0x7FFFFFF0 bytes (2 GiB); buffer skipped */
 #define RLE_STATUS_SERIAL      0x100u  /* info: stream decoded by the exact serial path (not encoder output) */
-#define RLE_STATUS_OPEN_TAIL   0x200u  /* info: the final token's count digit lies past C and reads as the zero
-                                          padding, so its byte fills up to U (not encoder output) */
 #define RLE_STATUS_SHORT       0x400u  /* info: the stream decodes to fewer than U bytes, the rest is zero
                                           (not encoder output) */
 

@@ -277,3 +277,17 @@ def test_full_size_shard_roundtrip_property():
         assert cl[i] == len(y)
         got = d_c[i * cap:i * cap + len(y)].cpu().numpy().tobytes()
         assert got == y, i
+
+
+@pytest.mark.parametrize("seg", [False, True])
+def test_decode_status_info_bits(seg):
+    # encoder output is status 0, including streams that end in a single 0x00 token (the reference
+    # reads it as a pair with the zero padding and fills to U with the zeros it already holds)
+    xs = [bytes(4096), b"ab\0", bytes(262144), b"q" * 100 + b"\0", O.gen(1, 3, 70000) + b"\0"]
+    ys, _ = gpu_encode(xs, seg=seg)
+    dec, st = gpu_decode(ys, [len(x) for x in xs], seg=seg)
+    assert dec == xs and (st == 0).all(), st
+    # streams that decode short of U: SHORT, the rest zero (src/rleCompression.c:48)
+    dec, st = gpu_decode([b"abc", b"ab\0", b"xx9" * 20000], [5, 7, 200000], seg=seg)
+    assert list(st) == [R.RLE_STATUS_SHORT] * 3, st
+    assert dec[0] == b"abc\0\0" and dec[1] == b"ab" + bytes(5) and dec[2] == b"x" * 180000 + bytes(20000)
