@@ -63,8 +63,21 @@ constexpr size_t kOneTripBytes = 128u << 10;
 constexpr size_t kSegEncodeBytes = 48u << 10;
 constexpr size_t kSegDecodeBytes = 32u << 10;
 
+// Host<->device transfers of large calls, selected by RLE_MI355X_STAGING:
+//   direct (default) the HIP runtime copies from / to the caller's pageable memory itself;
+//   pinned one memcpy into / out of this thread's pinned staging, one DMA;
+//   pipe   the pinned staging in chunks, the memcpy of one chunk overlapping the DMA of the next.
+// Calls below kPipeMinBytes always take "pinned" (one DMA each way).  Measured on MI355X
+// (profiles/r1d_staging.md): at 4 MiB, direct takes 231 / 255 us per compress / decompress call,
+// pinned 424 / 470, pipe 489 / 567; from 64 KiB to 1 MiB the three are within a few percent.
+enum class Staging { Pinned, Pipe, Direct };
+Staging g_staging = Staging::Direct;
+constexpr size_t kPipeMinBytes = 256u << 10;
+constexpr int kPipeEvents = 16;
+
 struct Ctx {
     int dev = 0;
+    hipEvent_t ev[kPipeEvents] = {};                 // chunk completion events of the pipelined D2H
     hipStream_t s = nullptr;
     uint8_t* h_in = nullptr;  size_t h_in_cap = 0;    // pinned staging: caller bytes -> device
     uint8_t* h_out = nullptr; size_t h_out_cap = 0;   // pinned staging: device -> caller block
@@ -114,6 +127,8 @@ void free_ctx(void* p) {
     (void)hipFree(c->d_ws);
     (void)hipFree(c->d_mid);
     (void)hipFree(c->d_bm);
+    for (hipEvent_t e : c->ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
     pthread_mutex_unlock(&g_exit_lock);
@@ -122,6 +137,10 @@ void free_ctx(void* p) {
 void init_once() {
     if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
+    if (const char* e = getenv("RLE_MI355X_STAGING")) {
+        if (!strcmp(e, "pinned")) g_staging = Staging::Pinned;
+        else if (!strcmp(e, "pipe")) g_staging = Staging::Pipe;
+    }
     pthread_key_create(&g_key, free_ctx);
     atexit(on_exit_handler);   // registered after the HIP runtime's own exit hooks: runs before them
 }
@@ -245,6 +264,120 @@ void warn_overflow(const char* who) {
                         "output truncated\n", who);
 }
 
+// Chunk size of the pipelined transfers: at least 256 KiB, at most kPipeEvents chunks.
+size_t pipe_chunk(size_t n) {
+    size_t ch = 256u << 10;
+    while ((n + ch - 1) / ch > (size_t)kPipeEvents) ch *= 2;
+    return ch;
+}
+
+// Queues the copy of n caller bytes at src to d_dst on c->s; src may be reused on return.
+void to_device(Ctx* c, uint8_t* d_dst, const void* src, size_t n) {
+    const uint8_t* p = static_cast<const uint8_t*>(src);
+    if (g_staging == Staging::Direct && n >= kPipeMinBytes) {
+        check(hipMemcpyAsync(d_dst, p, n, hipMemcpyHostToDevice, c->s), "H2D");
+        return;
+    }
+    grow_host(c->h_in, c->h_in_cap, n);
+    const size_t ch = (g_staging == Staging::Pipe && n >= kPipeMinBytes) ? pipe_chunk(n) : n;
+    for (size_t off = 0; off < n; off += ch) {
+        const size_t len = n - off < ch ? n - off : ch;
+        memcpy(c->h_in + off, p + off, len);
+        check(hipMemcpyAsync(d_dst + off, c->h_in + off, len, hipMemcpyHostToDevice, c->s), "H2D");
+    }
+}
+
+// Copies n device bytes at d_src (after everything queued on c->s) into the caller's dst; returns
+// with the stream drained up to that copy.
+void from_device(Ctx* c, void* dst, const uint8_t* d_src, size_t n) {
+    uint8_t* q = static_cast<uint8_t*>(dst);
+    if (n == 0) {
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        return;
+    }
+    if (g_staging == Staging::Direct && n >= kPipeMinBytes) {
+        check(hipMemcpyAsync(q, d_src, n, hipMemcpyDeviceToHost, c->s), "D2H");
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        return;
+    }
+    grow_host(c->h_out, c->h_out_cap, n);
+    if (g_staging != Staging::Pipe || n < kPipeMinBytes) {
+        check(hipMemcpyAsync(c->h_out, d_src, n, hipMemcpyDeviceToHost, c->s), "D2H");
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        memcpy(q, c->h_out, n);
+        return;
+    }
+    const size_t ch = pipe_chunk(n);
+    int k = 0;
+    for (size_t off = 0; off < n; off += ch, ++k) {
+        const size_t len = n - off < ch ? n - off : ch;
+        if (!c->ev[k]) check(hipEventCreateWithFlags(&c->ev[k], hipEventDisableTiming), "hipEventCreate");
+        check(hipMemcpyAsync(c->h_out + off, d_src + off, len, hipMemcpyDeviceToHost, c->s), "D2H");
+        check(hipEventRecord(c->ev[k], c->s), "hipEventRecord");
+    }
+    k = 0;
+    for (size_t off = 0; off < n; off += ch, ++k) {
+        const size_t len = n - off < ch ? n - off : ch;
+        check(hipEventSynchronize(c->ev[k]), "hipEventSynchronize");
+        memcpy(q + off, c->h_out + off, len);
+    }
+}
+
+// Small calls (one-wave kernels, output <= kOneTripBytes): the launch metadata travels inside the data
+// copies -- the input words after the caller's bytes in the one H2D, the output length / status
+// after the output slot in the one D2H -- so a call is one H2D, one launch, one D2H, one sync.
+constexpr size_t kMetaBytes = 64;
+
+// RLEcompress of U <= kOneTripBytes bytes; returns the caller's block.
+char* compress_small(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
+    const size_t Ur = round16(U), maxC = rle_max_compressed_size(U), Cr = round16(maxC);
+    grow_host(c->h_in, c->h_in_cap, Ur + kMetaBytes);
+    grow_host(c->h_out, c->h_out_cap, Cr + kMetaBytes);
+    grow_dev(c->d_in, c->d_in_cap, Ur + kMetaBytes);
+    grow_dev(c->d_out, c->d_out_cap, Cr + kMetaBytes);
+    memcpy(c->h_in, data, U);
+    uint64_t* hm = reinterpret_cast<uint64_t*>(c->h_in + Ur);
+    hm[0] = 0; hm[1] = U; hm[2] = 0;
+    check(hipMemcpyAsync(c->d_in, c->h_in, Ur + kMetaBytes, hipMemcpyHostToDevice, c->s), "H2D");
+    uint64_t* dm = reinterpret_cast<uint64_t*>(c->d_in + Ur);
+    uint64_t* dmo = reinterpret_cast<uint64_t*>(c->d_out + Cr);   // [C, status]
+    if (rle_encode_batch_device(c->d_in, dm + 0, dm + 1, c->d_out, dm + 2, dmo, reinterpret_cast<uint32_t*>(dmo + 1),
+                                1, c->s) != RLE_OK)
+        die("encode launch", hipGetLastError());
+    check(hipMemcpyAsync(c->h_out, c->d_out, Cr + kMetaBytes, hipMemcpyDeviceToHost, c->s), "D2H");
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const size_t C = reinterpret_cast<const uint64_t*>(c->h_out + Cr)[0];
+    return make_block(c, nullptr, 0, 0, C, compressedSize);
+}
+
+// RLEdecompress of C, U + E <= kOneTripBytes into the caller's block r (U + E bytes).
+void decompress_small(Ctx* c, const char* data, size_t C, size_t U, size_t E, char* r) {
+    const size_t total = U + E, Cr = round16(C), Tr = round16(total);
+    grow_host(c->h_in, c->h_in_cap, Cr + kMetaBytes);
+    grow_host(c->h_out, c->h_out_cap, Tr + kMetaBytes);
+    grow_dev(c->d_in, c->d_in_cap, Cr + kMetaBytes);
+    grow_dev(c->d_out, c->d_out_cap, Tr + kMetaBytes);
+    memcpy(c->h_in, data, C);
+    uint64_t* hm = reinterpret_cast<uint64_t*>(c->h_in + Cr);
+    hm[0] = 0; hm[1] = C; hm[2] = 0; hm[3] = U; hm[4] = total;
+    check(hipMemcpyAsync(c->d_in, c->h_in, Cr + kMetaBytes, hipMemcpyHostToDevice, c->s), "H2D");
+    uint64_t* dm = reinterpret_cast<uint64_t*>(c->d_in + Cr);
+    uint32_t* d_status = reinterpret_cast<uint32_t*>(c->d_out + Tr);
+    if (rle_decode_batch_device(c->d_in, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, dm + 4, d_status, 1, c->s) !=
+        RLE_OK)
+        die("decode launch", hipGetLastError());
+    check(hipMemcpyAsync(c->h_out, c->d_out, Tr + kMetaBytes, hipMemcpyDeviceToHost, c->s), "D2H");
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const uint32_t st = reinterpret_cast<const uint32_t*>(c->h_out + Tr)[0];
+    memcpy(r, c->h_out, U);
+    // the E region: zeros, unless a non-encoder stream wrote into it (it travelled with the rest)
+    if (E) {
+        if (st & RLE_STATUS_SERIAL) memcpy(r + U, c->h_out + U, E);
+        else memset(r + U, 0, E);
+    }
+    if (st & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompress");
+}
+
 }  // namespace
 
 // src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes.
@@ -255,17 +388,36 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
         return static_cast<char*>(calloc(16, 1));
     }
     Ctx* c = ctx();
-    grow_host(c->h_in, c->h_in_cap, U);
+    if (U < kSegEncodeBytes) {   // one wave walks it: the single-copy path
+        const uint64_t t0 = now_ns();
+        char* r = compress_small(c, data, U, compressedSize);
+        g_stats.calls_compress++;
+        g_stats.bytes_in += U;
+        g_stats.bytes_out += *compressedSize;
+        g_stats.bytes_h2d += round16(U) + kMetaBytes;
+        g_stats.bytes_d2h += round16(rle_max_compressed_size(U)) + kMetaBytes;
+        g_stats.ns_device += now_ns() - t0;
+        return r;
+    }
     grow_dev(c->d_in, c->d_in_cap, round16(U));
     const uint64_t t0 = now_ns();
-    memcpy(c->h_in, data, U);
+    to_device(c, c->d_in, data, U);
     const uint64_t t1 = now_ns();
-    check(hipMemcpyAsync(c->d_in, c->h_in, U, hipMemcpyHostToDevice, c->s), "H2D");
     const bool one_trip = queue_encode(c, c->d_in, U);
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-    const size_t C = fetch_encoded(c, one_trip, 0);
     const uint64_t t2 = now_ns();
-    char* r = make_block(c, nullptr, 0, 0, C, compressedSize);
+    const size_t C = c->h_meta[kMetaEnc + 3];
+    char* r;
+    if (one_trip) {
+        r = make_block(c, nullptr, 0, 0, C, compressedSize);
+    } else {   // the output travels now that C is known, straight into the caller's block
+        *compressedSize = C;
+        r = static_cast<char*>(malloc(C + 16));
+        if (r) {
+            from_device(c, r, c->d_out, C);
+            memset(r + C, 0, 16);
+        }
+    }
     const uint64_t t3 = now_ns();
     g_stats.calls_compress++;
     g_stats.bytes_in += U;
@@ -288,25 +440,32 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
         return r;
     }
     Ctx* c = ctx();
-    grow_host(c->h_in, c->h_in_cap, C);
-    grow_host(c->h_out, c->h_out_cap, total);
+    if (C < kSegDecodeBytes && total <= kOneTripBytes) {   // one wave walks it: the single-copy path
+        const uint64_t t0 = now_ns();
+        decompress_small(c, data, C, U, E, r);
+        g_stats.calls_decompress++;
+        g_stats.bytes_in += C;
+        g_stats.bytes_out += total;
+        g_stats.bytes_h2d += round16(C) + kMetaBytes;
+        g_stats.bytes_d2h += round16(total) + kMetaBytes;
+        g_stats.ns_device += now_ns() - t0;
+        return r;
+    }
     grow_dev(c->d_in, c->d_in_cap, round16(C));
     grow_dev(c->d_out, c->d_out_cap, round16(total));
     const uint64_t t0 = now_ns();
-    memcpy(c->h_in, data, C);
+    to_device(c, c->d_in, data, C);
     const uint64_t t1 = now_ns();
-    check(hipMemcpyAsync(c->d_in, c->h_in, C, hipMemcpyHostToDevice, c->s), "H2D");
     queue_decode(c, c->d_in, C, c->d_out, U, total);
-    if (U) check(hipMemcpyAsync(c->h_out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
-    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    from_device(c, r, c->d_out, U);   // also completes the status copy queued before it
     const uint32_t st = (uint32_t)c->h_meta[kMetaDec + 5];
     const uint64_t t2 = now_ns();
-    memcpy(r, c->h_out, U);
     if (E) {
         if (st & RLE_STATUS_SERIAL) {  // a non-encoder stream may have written into the E region
-            check(hipMemcpyAsync(c->h_out + U, c->d_out + U, E, hipMemcpyDeviceToHost, c->s), "D2H");
+            grow_host(c->h_out, c->h_out_cap, E);
+            check(hipMemcpyAsync(c->h_out, c->d_out + U, E, hipMemcpyDeviceToHost, c->s), "D2H");
             check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-            memcpy(r + U, c->h_out + U, E);
+            memcpy(r + U, c->h_out, E);
         } else {
             memset(r + U, 0, E);
         }
