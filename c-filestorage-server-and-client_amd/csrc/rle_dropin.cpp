@@ -271,19 +271,22 @@ size_t pipe_chunk(size_t n) {
     return ch;
 }
 
-// Queues the copy of n caller bytes at src to d_dst on c->s; src may be reused on return.
-void to_device(Ctx* c, uint8_t* d_dst, const void* src, size_t n) {
+// Queues the copy of n caller bytes at src to d_dst on c->s, staged (when staged) at h_in + hoff;
+// src may be reused on return.  Callers queuing several copies grow h_in for all of them first.
+void to_device(Ctx* c, uint8_t* d_dst, const void* src, size_t n, size_t hoff = 0) {
     const uint8_t* p = static_cast<const uint8_t*>(src);
+    if (n == 0) return;
     if (g_staging == Staging::Direct && n >= kPipeMinBytes) {
         check(hipMemcpyAsync(d_dst, p, n, hipMemcpyHostToDevice, c->s), "H2D");
         return;
     }
-    grow_host(c->h_in, c->h_in_cap, n);
+    grow_host(c->h_in, c->h_in_cap, hoff + n);
+    uint8_t* h = c->h_in + hoff;
     const size_t ch = (g_staging == Staging::Pipe && n >= kPipeMinBytes) ? pipe_chunk(n) : n;
     for (size_t off = 0; off < n; off += ch) {
         const size_t len = n - off < ch ? n - off : ch;
-        memcpy(c->h_in + off, p + off, len);
-        check(hipMemcpyAsync(d_dst + off, c->h_in + off, len, hipMemcpyHostToDevice, c->s), "H2D");
+        memcpy(h + off, p + off, len);
+        check(hipMemcpyAsync(d_dst + off, h + off, len, hipMemcpyHostToDevice, c->s), "H2D");
     }
 }
 
@@ -378,6 +381,60 @@ void decompress_small(Ctx* c, const char* data, size_t C, size_t U, size_t E, ch
     if (st & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompress");
 }
 
+}  // namespace
+
+int rle_append_prepare_launch(const void* d_mid, uint64_t U, void* d_head, unsigned long long* d_start,
+                              uint64_t* d_res, hipStream_t s);   // csrc/rle_fileops.hip
+
+namespace {
+// RLEappend of a small file (old stream decoded by one wave, c^r ‖ new encoded by one wave, output
+// within kOneTripBytes) in one H2D and one D2H:
+//   d_in  = [old stream | splice head (16) | new bytes | launch words]
+//   d_out = [re-encoded tail | result words: C', encode status, decode status, r, head (2)]
+// Returns false (and leaves nothing but d_mid's decoded old content behind) when the final-token
+// check fails and the caller must re-encode whole; *Ce / *r then are meaningless.
+constexpr size_t kAppendWords = 16;
+bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* add, size_t A, size_t* Ce,
+                  size_t* r) {
+    const size_t Cr = round16(C), Ar = round16(A), offW = Cr + 16 + Ar, inBytes = offW + 8 * kAppendWords;
+    const size_t Er = round16(rle_max_compressed_size(16 + A)), outBytes = Er + 64;
+    grow_host(c->h_in, c->h_in_cap, inBytes);
+    grow_host(c->h_out, c->h_out_cap, outBytes);
+    grow_dev(c->d_in, c->d_in_cap, inBytes);
+    grow_dev(c->d_out, c->d_out_cap, outBytes);
+    grow_dev(c->d_mid, c->d_mid_cap, round16(U + A));
+    memcpy(c->h_in, content, C);
+    if (A) memcpy(c->h_in + Cr + 16, add, A);
+    uint64_t* hw = reinterpret_cast<uint64_t*>(c->h_in + offW);
+    hw[0] = 0; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = U;   // decode: in_off, in_len, out_off, out_len, cap
+    hw[5] = Cr; hw[6] = 16 + A; hw[7] = 0;                  // encode: in_off, in_len, out_off
+    hw[8] = 0;                                               // final-run start accumulator
+    check(hipMemcpyAsync(c->d_in, c->h_in, inBytes, hipMemcpyHostToDevice, c->s), "H2D");
+    uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_in + offW);
+    uint64_t* res = reinterpret_cast<uint64_t*>(c->d_out + Er);
+    if (rle_decode_batch_device(c->d_in, dw + 0, dw + 1, c->d_mid, dw + 2, dw + 3, dw + 4,
+                                reinterpret_cast<uint32_t*>(res + 2), 1, c->s) != RLE_OK)
+        die("decode launch", hipGetLastError());
+    if (rle_append_prepare_launch(c->d_mid, U, c->d_in + Cr, reinterpret_cast<unsigned long long*>(dw + 8), res + 3,
+                                  c->s) != RLE_OK)
+        die("append launch", hipGetLastError());
+    if (rle_encode_batch_device(c->d_in, dw + 5, dw + 6, c->d_out, dw + 7, res + 0, reinterpret_cast<uint32_t*>(res + 1),
+                                1, c->s) != RLE_OK)
+        die("encode launch", hipGetLastError());
+    check(hipMemcpyAsync(c->h_out, c->d_out, outBytes, hipMemcpyDeviceToHost, c->s), "D2H");
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const uint64_t* hr = reinterpret_cast<const uint64_t*>(c->h_out + Er);
+    const uint32_t st = (uint32_t)hr[2];
+    const size_t rr = hr[3];
+    const uint8_t ch = reinterpret_cast<const uint8_t*>(hr + 4)[15];
+    const uint8_t* y = reinterpret_cast<const uint8_t*>(content);
+    const size_t tok = rr == 1 ? 1 : 3;
+    bool ok = st == RLE_STATUS_OK && rr >= 1 && rr <= 9 && C >= tok && y[C - tok] == ch;
+    if (ok && tok == 3) ok = y[C - 2] == ch && y[C - 1] == (uint8_t)('0' + rr);
+    *Ce = hr[0];
+    *r = rr;
+    return ok;
+}
 }  // namespace
 
 // src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes.
@@ -492,17 +549,39 @@ extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompresse
     // overwritten by the appended bytes (:767-770), so the result is encode(newContent)
     if (U == 0) return RLEcompress(const_cast<char*>(newContent), A, newCompressedSize);
     Ctx* c = ctx();
+    if (C && C < kSegDecodeBytes && 16 + A < kSegEncodeBytes &&
+        rle_max_compressed_size(16 + A) <= kOneTripBytes) {
+        const uint64_t t0 = now_ns();
+        size_t Ce = 0, r = 0;
+        char* out = nullptr;
+        if (append_small(c, content, C, U, newContent, A, &Ce, &r)) {
+            const size_t skip = 16 - r;
+            out = make_block(c, content, C - (r == 1 ? 1 : 3), skip, Ce, newCompressedSize);
+        } else {   // not encoder output: re-encode decode(old) ‖ new whole, as the reference does
+            if (A) check(hipMemcpyAsync(c->d_mid + U, c->d_in + round16(C) + 16, A, hipMemcpyDeviceToDevice, c->s),
+                         "D2D");
+            const bool one_trip = queue_encode(c, c->d_mid, U + A);
+            check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+            const size_t Cn = fetch_encoded(c, one_trip, 0);
+            out = make_block(c, nullptr, 0, 0, Cn, newCompressedSize);
+        }
+        g_stats.calls_append++;
+        g_stats.bytes_in += C + A;
+        g_stats.bytes_out += *newCompressedSize;
+        g_stats.bytes_h2d += round16(C) + 16 + round16(A) + 8 * kAppendWords;
+        g_stats.bytes_d2h += round16(rle_max_compressed_size(16 + A)) + 64;
+        g_stats.ns_device += now_ns() - t0;
+        return out;
+    }
     const size_t offA = round16(C) + 16;   // d_in: old stream | splice head (16 B) | new bytes
     const size_t inBytes = offA + A;
     grow_host(c->h_in, c->h_in_cap, inBytes);
     grow_dev(c->d_in, c->d_in_cap, round16(inBytes));
     grow_dev(c->d_mid, c->d_mid_cap, round16(U + A));
     const uint64_t t0 = now_ns();
-    if (C) memcpy(c->h_in, content, C);
-    if (A) memcpy(c->h_in + offA, newContent, A);
+    to_device(c, c->d_in, content, C, 0);
+    to_device(c, c->d_in + offA, newContent, A, offA);
     const uint64_t t1 = now_ns();
-    if (C) check(hipMemcpyAsync(c->d_in, c->h_in, C, hipMemcpyHostToDevice, c->s), "H2D");
-    if (A) check(hipMemcpyAsync(c->d_in + offA, c->h_in + offA, A, hipMemcpyHostToDevice, c->s), "H2D");
     bool full = C == 0;   // no stream: the decoded content is U zero bytes (:48), re-encoded whole
     bool one_trip = false;
     if (full) {

@@ -49,10 +49,10 @@ __global__ __launch_bounds__(256) void last_run_kernel(const uint8_t* __restrict
 // Splice head: head[0, 16) = (16 - r) filler bytes ‖ c^r, with r = ((U - start) - 1) % 9 + 1.
 // The filler alternates c^1, c^2 (adjacent bytes differ, none equals c), so it encodes to
 // itself, one single-byte token per byte, and the head's final r bytes start a fresh run:
-// encode(head ‖ new) = filler ‖ encode(c^r ‖ new).  meta[1] = r, meta[2..3] = the head.
+// encode(head ‖ new) = filler ‖ encode(c^r ‖ new).  res[0] = r, res[1..2] = a copy of the head.
 __global__ void splice_head_kernel(const uint8_t* __restrict__ mid, uint64_t U,
                                    const unsigned long long* __restrict__ start, uint8_t* __restrict__ head,
-                                   uint64_t* __restrict__ meta) {
+                                   uint64_t* __restrict__ res) {
     const uint32_t lane = threadIdx.x;
     const uint8_t c = mid[U - 1];
     const uint64_t L = U - *start;
@@ -60,24 +60,32 @@ __global__ void splice_head_kernel(const uint8_t* __restrict__ mid, uint64_t U,
     if (lane < 16) {
         const uint8_t v = lane >= 16 - r ? c : (uint8_t)(c ^ ((lane & 1) ? 2 : 1));
         head[lane] = v;
-        reinterpret_cast<uint8_t*>(meta + 2)[lane] = v;
+        reinterpret_cast<uint8_t*>(res + 1)[lane] = v;
     }
-    if (lane == 0) meta[1] = r;
+    if (lane == 0) res[0] = r;
 }
 
 }  // namespace rle
+
+// Both kernels of rle_append_prepare_device, with the run-start accumulator (*d_start, zero on
+// entry) and the results (res[0] = r, res[1..2] = head) where the caller wants them (the drop-in
+// keeps them inside its single-copy call buffers).  Not in the public headers.
+int rle_append_prepare_launch(const void* d_mid, uint64_t U, void* d_head, unsigned long long* d_start,
+                              uint64_t* d_res, hipStream_t s) {
+    const uint64_t nchunks = (U + 15) / 16;
+    uint64_t blocks = (nchunks + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(rle::last_run_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint8_t*)d_mid, U,
+                       d_start);
+    hipLaunchKernelGGL(rle::splice_head_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_mid, U, d_start,
+                       (uint8_t*)d_head, d_res);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
 
 extern "C" int rle_append_prepare_device(const void* d_mid, uint64_t U, void* d_head, uint64_t* d_meta,
                                          void* stream) {
     if (U == 0 || !d_mid || !d_head || !d_meta) return RLE_E_INVAL;
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_meta, 0, sizeof(uint64_t), s) != hipSuccess) return RLE_E_HIP;
-    const uint64_t nchunks = (U + 15) / 16;
-    uint64_t blocks = (nchunks + 255) / 256;
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(rle::last_run_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint8_t*)d_mid, U,
-                       reinterpret_cast<unsigned long long*>(d_meta));
-    hipLaunchKernelGGL(rle::splice_head_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_mid, U,
-                       reinterpret_cast<const unsigned long long*>(d_meta), (uint8_t*)d_head, d_meta);
-    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+    return rle_append_prepare_launch(d_mid, U, d_head, reinterpret_cast<unsigned long long*>(d_meta), d_meta + 1, s);
 }
