@@ -206,8 +206,9 @@ __device__ __forceinline__ void walk_prime(u32x4 rs, u32 start, u32 ntiles, u32 
     if (ntiles) dma_tile(rs, lo, l0);
     if (ntiles > 1u) dma_tile(rs, kTileStep + lo, l1);
 }
+// Returns whether a step stopped the walk (~0u).
 template <class Step>
-__device__ __forceinline__ void walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots,
+__device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots,
                                            Step step, bool primed = false) {
     const u32 lo = start + 16u * lane;
     const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
@@ -223,7 +224,7 @@ __device__ __forceinline__ void walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
         p1 = step(t, slots, Refill{rs, (t + 2u) * kTileStep + lo, l0, t + 2u < ntiles});
         if (p1 == ~0u) {
             vm_drain();
-            return;
+            return true;
         }
         if (t + 1u >= ntiles) break;
         vm_wait(p2 + (t + 2u < ntiles ? 1u : 0u) + p1);
@@ -231,9 +232,10 @@ __device__ __forceinline__ void walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
         p1 = step(t + 1u, slots + kSlot, Refill{rs, (t + 3u) * kTileStep + lo, l1, t + 3u < ntiles});
         if (p1 == ~0u) {
             vm_drain();
-            return;
+            return true;
         }
     }
+    return false;
 }
 __device__ __forceinline__ u32 ntiles_for(u32 n) { return (n + kTileStep - 1u) / kTileStep; }
 
@@ -560,7 +562,6 @@ struct DecState {
     u32 d;         // offset of the first token start in the current tile (0..2)
     u32 fillc;     // byte of the last stored position (run continuation carry)
     u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
-    u32 serial;    // 1 -> stream needs the exact serial path
     u32 head;      // leading bytes of the first stored chunk that belong to the previous segment
     u32 prev;      // stream byte before the current tile, in bits 24..31
     Stamps sp;     // diagnostic builds only
@@ -799,8 +800,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32 ttot = readlane(oincl, kOwnLanes - 1u);
     constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
     if ((__builtin_amdgcn_ballot_w64(ln.serial_lane) & kOwned) || st.out_pos + ttot > U) {
-        st.serial = 1;
-        return ~0u;
+        return ~0u;   // the stream needs the exact serial path
     }
     if (pr.tail) {
         const uint64_t pfb = __builtin_amdgcn_ballot_w64(ln.PF != 0u) & kOwned;

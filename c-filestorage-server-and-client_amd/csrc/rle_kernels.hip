@@ -145,12 +145,12 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             return;
         }
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, {}};
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, {}};
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
         st.sp.last = memtime();
 #endif
-        walk_tiles(
+        const bool serial = walk_tiles(
             rsi, 0u, ntiles, lane, slots,
             [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st);
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             true);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
-        if (st.serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
+        if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
         else {
             dec_finish(st, U, lane, stage, rso, dst);
             stat = dec_tiled_status(st, U);

@@ -407,13 +407,13 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         const u32 e = uniform(pl.x), off = uniform(pl.y);
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{off, off & ~15u, e, 0u, 0u, 0u, off & 15u, 0u, {}};
-        walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, {}};
+        const bool serial = walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
             return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st);
         });
         const bool last = g + 1u == s0 + nseg;
         dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
-        if (last && lane == 0 && status) status[b] = st.serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : dec_tiled_status(st, U);
+        if (last && lane == 0 && status) status[b] = serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : dec_tiled_status(st, U);
     }
 }
 
