@@ -451,19 +451,31 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
         }
     }
     RLE_STAMP(st.sp, 2);   // pass 1
-    // pass 2: second byte and count digit of each 3-byte token, written from the token's own
-    // tile (its second input byte may sit in the next tile, after this tile's flush)
+    // pass 2: the count digit of each 3-byte token, '0' + min(9, run left), at its start + 2.
+    // (Pass 1 already wrote every token's second byte from the position holding it, except where
+    // that position lies past the wave's owned range: those few are written after the loop.)
+    const u32 obase = 16u + rel0 + oincl - nout;
     u32 prem = (RLE_EABL & 2) ? 0u : P;
     while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
         if (prem) {
             const u32 j = (u32)__builtin_ctz(prem);
             prem &= prem - 1u;
             const u32 mj = lowmask(j);
-            const u32 oj = 16u + rel0 + oincl - nout + bcnt(T & mj, 0u) + 2u * bcnt(P & mj, 0u);
-            const u32 rem = (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u) + 1u;   // min(9, run left)
+            const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+            stage[oj + 2u] = (uint8_t)('1' + (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u));
+        }
+    }
+    // second bytes whose position is not owned here (the lane's last valid position, when the
+    // next one belongs to the next tile, segment or nothing)
+    const u32 vnext = (validm >> 1) | ((from_next_lane(validm, 0u) & 1u) << 15);
+    const u32 PX = (RLE_EABL & 2) ? 0u : (P & ~vnext);
+    if (__builtin_amdgcn_ballot_w64(PX != 0u)) {
+        if (PX) {
+            const u32 j = (u32)__builtin_ctz(PX);
+            const u32 mj = lowmask(j);
+            const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
             const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
             stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
-            stage[oj + 2u] = (uint8_t)('0' + rem);
         }
     }
     wave_lds_sync();
