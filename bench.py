@@ -186,12 +186,19 @@ def main():
     stream = torch.cuda.current_stream()
 
     B = Batch(wl, rank, world, dev)
+    comm = torch.cuda.Stream(device=dev) if world > 1 else None
 
     def step():
         B.encode(stream)
-        if world > 1:   # the one exchange step: sizes all-gathered over RCCL, scanned in global order
-            shard.global_offsets(B.clen, world)
+        if world > 1:
+            # the one exchange step: sizes all-gathered over RCCL and scanned in global order, on
+            # its own stream so it overlaps the decode (which does not need the global offsets)
+            comm.wait_stream(stream)
+            with torch.cuda.stream(comm):
+                shard.global_offsets(B.clen, world)
         B.decode(stream)
+        if world > 1:
+            stream.wait_stream(comm)   # the next encode rewrites the sizes the gather reads
 
     for _ in range(max(1, args.warmup)):
         step()
