@@ -604,20 +604,20 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         const u32 c = k * kWave + lane;
         const bool active = c < nfl;
         u32x4* s4 = reinterpret_cast<u32x4*>(stage + 32u * (c + 1u));
-        u32x4 a = u32x4{0u, 0u, 0u, 0u}, b = a;
-        if (active) {
-            if (RLE_SWZ == 1) {
-                const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
-                auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
-                a = u32x4{rd(0), rd(1), rd(2), rd(3)};
-                b = u32x4{rd(4), rd(5), rd(6), rd(7)};
-            } else if (RLE_SWZ == 2) {
-                a = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4)));
-                b = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4) + 16u));
-            } else {
-                a = s4[0];
-                b = s4[1];
-            }
+        // read unconditionally: an inactive lane's chunk (at most one past this wave's staging)
+        // is garbage it never stores, and LDS reads do not fault
+        u32x4 a, b;
+        if (RLE_SWZ == 1) {
+            const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
+            auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
+            a = u32x4{rd(0), rd(1), rd(2), rd(3)};
+            b = u32x4{rd(4), rd(5), rd(6), rd(7)};
+        } else if (RLE_SWZ == 2) {
+            a = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4)));
+            b = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4) + 16u));
+        } else {
+            a = s4[0];
+            b = s4[1];
         }
         RLE_STAMP(sp, 3);   // flush: staging reads
         // position index p (bits 8..11 of each u16) into each key; empty slots get the index alone,
@@ -675,8 +675,17 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
 // maps.  Positions are absolute in the stream; tokens start only below Co (the end of the
 // positions this wave owns: the stream, or its segment).  Lane 63 holds only the next tile's first
 // 16 bytes (lookahead): its results are garbage and every consumer ignores it.
+// Register constants of the decode tile, made once per kernel (vconst: no rematerialisation
+// inside the tile loop).
+struct DecK {
+    u32 K80, K7F, C1, C2;
+};
+__device__ __forceinline__ DecK dec_k() {
+    return DecK{vconst(0x80808080u), vconst(0x7F7F7F7Fu), vconst(0x08040201u), vconst(0x80402010u)};
+}
 struct DecPrep {
     u32 w[4], g[4];
+    u32 K80;
     u32 la;        // next lane's first 4 bytes (count digits of positions 14, 15)
     u32 left;      // stream bytes from the lane's first position
     u32 lefto;     // owned positions from the lane's first position
@@ -686,8 +695,9 @@ struct DecPrep {
     bool tail;     // the tile reaches the owned end or the stream end (validity masks needed)
 };
 __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, u32 Co, u32 lane,
-                                               const DecEntry* tbl) {
+                                               const DecEntry* tbl, const DecK& kc) {
     DecPrep r;
+    r.K80 = kc.K80;
     const u32 p0 = pos + 16u * lane;
     r.left = p0 < C ? C - p0 : 0u;
     r.lefto = p0 < Co ? Co - p0 : 0u;
@@ -704,17 +714,17 @@ __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, 
     }
     const u32 la = from_next_lane(w[0], 0u);
     r.la = la;
-    const u32 K80 = vconst(0x80808080u);
+    const u32 K80 = kc.K80;
     const u32 nx[4] = {alignbyte(w[1], w[0], 1), alignbyte(w[2], w[1], 1), alignbyte(w[3], w[2], 1),
                        alignbyte(la, w[3], 1)};
-    const u32 K7F = vconst(0x7F7F7F7Fu);   // in a VGPR: v_bitop3 with an SGPR operand is slow-class
+    const u32 K7F = kc.K7F;   // in a VGPR: v_bitop3 with an SGPR operand is slow-class
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 t = w[k] ^ nx[k];
         const u32 u = faddi<0x7F7F7F7Fu>(t & K7F);
         r.g[k] = bitop3<kOrAnd>(u, t, K80);
     }
-    const u32 C1 = vconst(0x08040201u), C2 = vconst(0x80402010u);
+    const u32 C1 = kc.C1, C2 = kc.C2;
     r.xa = __builtin_amdgcn_udot4(r.g[1], C2, __builtin_amdgcn_udot4(r.g[0], C1, 0u, false), false);
     r.xb = __builtin_amdgcn_udot4(r.g[3], C2, __builtin_amdgcn_udot4(r.g[2], C1, 0u, false), false);
     const u32 tbase = lds_addr(tbl);
@@ -740,14 +750,17 @@ struct DecLen {
 __device__ __forceinline__ u32 expand80(u32 m16, u32 k, u32 K80) {
     return __umul24(bfe(m16, 4u * k, 4) << 7, 0x00204081u) & K80;
 }
-__device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
+// kTail: the tile reaches the owned end or the stream end (p.tail); instantiated separately so the
+// common tiles use the masks' constant values directly.
+template <bool kTail>
+__device__ __forceinline__ DecLen dec_lengths_t(const DecPrep& p, u32 d) {
     DecLen r;
     const u32* w = p.w;
     const u32 dl = bfe(p.excl, 8u * d, 8);                                    // lane entry phase
     const u32 mid = __builtin_amdgcn_perm(0u, p.ta.y, 0x0C0C0C00u | dl);      // phase entering position 8
     const u32 sa = __builtin_amdgcn_perm(0u, p.ta.x, 0x0C0C0C00u | dl);       // start bits 0..7
     const u32 sb = __builtin_amdgcn_perm(0u, p.tb.x, 0x0C0C0C00u | mid);      // start bits 8..15
-    const u32 K80 = vconst(0x80808080u);
+    const u32 K80 = p.K80;
     const u32 sa7 = sa << 7, sb7 = sb << 7;
     u32 S80[4] = {__umul24(sa7 & 0x780u, 0x00204081u) & K80,
                   __umul24((sa7 >> 4) & 0x780u, 0x00204081u) & K80,
@@ -759,7 +772,7 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     u32 O02[4] = {0x02020202u, 0x02020202u, 0x02020202u, 0x02020202u};   // 2 at owned positions
     r.PF = 0u;
     bool sf = false;
-    if (p.tail) {
+    if (kTail) {
         // owned: j < lefto; digit inside the stream: j + 2 < left; second byte inside: j + 1 < left
         const u32 lo16 = lowmask(p.lefto < 16u ? p.lefto : 16u);
         const u32 l18 = lowmask(p.left < 18u ? p.left : 18u);
@@ -798,14 +811,17 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     r.serial_lane = (bad & K80) != 0u || sf;
     return r;
 }
+__device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
+    return p.tail ? dec_lengths_t<true>(p, d) : dec_lengths_t<false>(p, d);
+}
 
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
                                         u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
-                                        DecState& st) {
+                                        DecState& st, const DecK& kc) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
-    const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl);
+    const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
     const DecLen ln = dec_lengths(pr, st.d);
     const u32* w = pr.w;
     const u32 oincl = wave_scan_incl(ln.nout, 0u, OpAdd());

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         }
         const u32x4 rso = make_rsrc(dst, U);
         DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, {}};
+        const DecK kc = dec_k();
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
         st.sp.last = memtime();
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         const bool serial = walk_tiles(
             rsi, 0u, ntiles, lane, slots,
             [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st);
+                return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc);
             },
             true);
         RLE_STAMP(st.sp, 7);   // drain after the last tile

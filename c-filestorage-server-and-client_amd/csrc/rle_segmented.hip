@@ -275,10 +275,11 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_
             seg_range(g - s0, nseg, C, sb, q0, q1);
             const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
             u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
+            const DecK kc = dec_k();
             walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
                 nx();
-                const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl);
+                const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
                 const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
                 if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
                     const DecLen ln = dec_lengths(pr, d0);
@@ -408,8 +409,9 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
         DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, {}};
+        const DecK kc = dec_k();
         const bool serial = walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st);
+            return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc);
         });
         const bool last = g + 1u == s0 + nseg;
         dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
