@@ -350,8 +350,13 @@ struct EncAn {
     u32 w[4];
     u32 p0, validm, top, B, B24, incl, T, P;
 };
+// Register constants of the encode tile, made once per kernel (vconst: no rematerialisation).
+struct EncK {
+    u32 K80, C1, C2;
+};
+__device__ __forceinline__ EncK enc_k() { return EncK{vconst(0x80808080u), vconst(0x08040201u), vconst(0x80402010u)}; }
 __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u32 Uo, u32 lane, u32 prev_top,
-                                             u32 rs) {
+                                             u32 rs, const EncK& kc) {
     EncAn a;
     a.w[0] = cur.x; a.w[1] = cur.y; a.w[2] = cur.z; a.w[3] = cur.w;
     const u32* w = a.w;
@@ -369,14 +374,14 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
     const u32 ptop = from_prev_lane(top, prev_top);
     const u32 pw[4] = {alignbyte(w[0], ptop, 3), alignbyte(w[1], w[0], 3), alignbyte(w[2], w[1], 3),
                        alignbyte(w[3], w[2], 3)};
-    const u32 K80 = vconst(0x80808080u);
+    const u32 K80 = kc.K80;
     u32 g[4];   // 0x80 per byte that differs from the byte before it
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 t = w[k] ^ pw[k];
         g[k] = bitop3<kOrAnd>(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu), t, K80);
     }
-    const u32 C1 = vconst(0x08040201u), C2 = vconst(0x80402010u);
+    const u32 C1 = kc.C1, C2 = kc.C2;
     const u32 Ba = __builtin_amdgcn_udot4(g[1], C2, __builtin_amdgcn_udot4(g[0], C1, 0u, false), false);
     const u32 Bb = __builtin_amdgcn_udot4(g[3], C2, __builtin_amdgcn_udot4(g[2], C1, 0u, false), false);
     u32 B = (Ba >> 7) | (Bb + Bb);
@@ -406,11 +411,12 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
 }
 
 __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
-                                        u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st) {
+                                        u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
+                                        const EncK& kc) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
-    const EncAn an = enc_analyze(cur, pos, Ud, Uo, lane, st.prev_top, st.rs);
+    const EncAn an = enc_analyze(cur, pos, Ud, Uo, lane, st.prev_top, st.rs, kc);
     const u32* w = an.w;
     const u32 validm = an.validm, top = an.top, B24 = an.B24, incl = an.incl, T = an.T, P = an.P;
 
@@ -487,8 +493,9 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
-        u32x4 v = u32x4{0u, 0u, 0u, 0u};
-        if (c < nfl) v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
+        // read unconditionally: an inactive lane's chunk (at most one past this wave's staging) is
+        // garbage it never stores, and LDS reads do not fault
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
         const bool skip = st.head && c == 0u;   // shared with the previous segment: byte stores below
         vstore(rso, (c < nfl && !skip && !(RLE_EABL & 4)) ? st.flushed + 16u * c : kOOB, v);
         if (skip && nfl) {

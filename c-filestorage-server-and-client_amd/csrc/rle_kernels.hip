@@ -61,12 +61,13 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
     EncState st{0u, 0u, 0u, 0u, 0u, {}};
+    const EncK kc = enc_k();
 #if RLE_STAMPS
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
     st.sp.last = memtime();
 #endif
     walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-        return enc_tile(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st);
+        return enc_tile(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc);
     });
     RLE_STAMP(st.sp, 6);   // drain
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
