@@ -109,3 +109,31 @@ def test_decompress_n_readn_batch_of_fixture_files(dummyfiles):
     xs = [x for x in (committed_file_bytes(e) for e in dummyfiles["files"]) if x is not None]
     ys = [R.compress(x) for x in xs]
     assert R.decompress_n(ys, [len(x) for x in xs]) == xs
+
+
+def test_fileops_concurrent_threads():
+    """The server's worker pool calls these from many threads at once (src/server.c:520-524)."""
+    import threading
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(100 + t)
+        content, plain = b"", b""
+        for k in range(25):
+            new = O.gen(int(rng.integers(0, 5)), t * 100 + k, int(rng.integers(0, 40000)))
+            content = R.append(content, len(plain), new)
+            plain += new
+            if content != O.encode(plain):
+                errors.append(("append", t, k))
+                return
+            if k % 5 == 4:
+                xs = [plain[: len(plain) // 3], plain, new]
+                if R.decompress_n([O.encode(x) for x in xs], [len(x) for x in xs]) != xs:
+                    errors.append(("readN", t, k))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
