@@ -410,6 +410,34 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
     return a;
 }
 
+// Pass 1 of enc_tile: every position writes its byte at its token's offset (starts) or at
+// offset-2 of the next token (valid non-starts: its own token's second byte, a redundant identical
+// write); positions past U write at the tile's output end, which is never stored.  e0 = staging
+// address of the lane's first output byte; byte i of Q = output bytes of positions >= i of the
+// dword (suffix sums by right shifts), so position i writes at endk - Q.byte_i (- 2).  kFull: all
+// 16 positions of every owned lane are valid, so the non-starts are V01 - T01 (V01 = 0x01010101 on
+// lanes 0..62, 0 on the lookahead lane) without an expansion of their own.
+template <bool kFull>
+__device__ __forceinline__ void enc_pass1(const u32* w, u32 T, u32 P, u32 NS, u32 e0, u32 V01) {
+    u32 endk = e0;
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 T01 = nib_to_bytes(bfe(T, 4u * k, 4)), P01 = nib_to_bytes(bfe(P, 4u * k, 4));
+        const u32 N01 = kFull ? V01 - T01 : nib_to_bytes(bfe(NS, 4u * k, 4));
+        const u32 W = T01 + P01 + P01;
+        u32 Q = W + (W >> 8);
+        Q = Q + (Q >> 16);
+        endk = endk + (Q & 0xFFu);
+        const u32 R = Q + N01 + N01;
+        auto put = [](u32 t, u32 v) { *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(t) = (uint8_t)v; };
+        const u32 w8 = w[k] >> 8;
+        put(sub_byte<0>(endk, R), w[k]);
+        put(sub_byte<1>(endk, R), w8);
+        put(sub_byte<2>(endk, R), w[k] >> 16);
+        put(sub_byte<3>(endk, R), w8 >> 16);
+    }
+}
+
 __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
                                         u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
                                         const EncK& kc) {
@@ -437,24 +465,10 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
 #endif
     // staging byte address after this lane's output; byte i of Q = output bytes of positions >= i
     // of the dword (suffix sums by right shifts), so position i writes at endk - Q.byte_i (- 2)
-    u32 endk = lds_addr(stage) + 16u + rel0 + oincl - nout;
     if (!(RLE_EABL & 1)) {
-#pragma unroll
-        for (u32 k = 0; k < 4; ++k) {
-            const u32 T01 = nib_to_bytes(bfe(T, 4u * k, 4)), P01 = nib_to_bytes(bfe(P, 4u * k, 4));
-            const u32 N01 = nib_to_bytes(bfe(NS, 4u * k, 4));
-            const u32 W = T01 + P01 + P01;
-            u32 Q = W + (W >> 8);
-            Q = Q + (Q >> 16);
-            endk = endk + (Q & 0xFFu);
-            const u32 R = Q + N01 + N01;
-            auto put = [](u32 t, u32 v) { *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(t) = (uint8_t)v; };
-            const u32 w8 = w[k] >> 8;
-            put(sub_byte<0>(endk, R), w[k]);
-            put(sub_byte<1>(endk, R), w8);
-            put(sub_byte<2>(endk, R), w[k] >> 16);
-            put(sub_byte<3>(endk, R), w8 >> 16);
-        }
+        const u32 e0 = lds_addr(stage) + 16u + rel0 + oincl - nout;
+        if (pos + kTileStep <= Uo) enc_pass1<true>(w, T, P, NS, e0, lane < kOwnLanes ? 0x01010101u : 0u);
+        else enc_pass1<false>(w, T, P, NS, e0, 0u);
     }
     RLE_STAMP(st.sp, 2);   // pass 1
     // pass 2: the count digit of each 3-byte token, '0' + min(9, run left), at its start + 2.
