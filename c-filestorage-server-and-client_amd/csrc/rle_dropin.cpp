@@ -5,12 +5,16 @@
 // re-encode) and src/server.c:317 (evicted files), which link against this library unchanged.
 //
 // Each calling thread (the server's worker pool, src/server.c:520-524) gets its own HIP stream,
-// pinned host staging and device buffers, created lazily on its first call (there is no init
-// hook in the server, src/server.c:406-524) and released at thread exit.  A call is: copy the
-// caller's bytes into pinned staging -> H2D -> one batched kernel launch with B = 1 -> D2H ->
-// copy into a fresh malloc() block, which is what the callers free() (src/filesystemApi.c:208,
+// pinned host buffers and device buffers, created lazily on its first call (there is no init
+// hook in the server, src/server.c:406-524) and released at thread exit.  A call is one batched
+// kernel launch with B = 1 plus the host<->device traffic, sized to the call:
+//   small (one wave walks it)  zero-copy on the thread's mapped pinned buffer, one launch, one sync;
+//   medium                     one H2D / one D2H through pinned staging, segmented kernels;
+//   large (>= 256 KiB)         the runtime copies straight from / to the caller's memory.
+// The result is a fresh malloc() block, which is what the callers free() (src/filesystemApi.c:208,
 // 687, 775, 811; src/server.c:269, 320).  There is no CPU codec in this library: without a
-// usable GPU it reports the problem and aborts.
+// usable GPU it reports the problem and aborts.  RLEappend / RLEdecompressN (include/
+// rle_fileops.h) are the fused and batched forms of the callers' compositions.
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <errno.h>
