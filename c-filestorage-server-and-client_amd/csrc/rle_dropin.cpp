@@ -341,9 +341,11 @@ void from_device(Ctx* c, void* dst, const uint8_t* d_src, size_t n) {
     }
 }
 
-// Small calls (one-wave kernels, output <= kOneTripBytes): the launch metadata travels inside the data
-// copies -- the input words after the caller's bytes in the one H2D, the output length / status
-// after the output slot in the one D2H -- so a call is one H2D, one launch, one D2H, one sync.
+// Small calls (one-wave kernels, output <= kOneTripBytes).  Zero-copy (default): the caller's bytes,
+// the launch words and the result live in the thread's mapped pinned buffer (kZc* layout).  Copying
+// (RLE_MI355X_SMALL=copy): the launch words travel inside the data copies -- the input words after
+// the caller's bytes in the one H2D, the output length / status after the output slot in the one
+// D2H -- so a call is one H2D, one launch, one D2H, one sync.
 constexpr size_t kMetaBytes = 64;
 
 uint8_t* zc(Ctx* c) {
