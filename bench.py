@@ -186,19 +186,28 @@ def main():
     stream = torch.cuda.current_stream()
 
     B = Batch(wl, rank, world, dev)
+    # N > 1: the one exchange step -- each step's compressed sizes all-gathered over RCCL and
+    # scanned into global stream offsets -- runs on its own stream, off the codec's critical path.
+    # The sizes are copied into one of two buffers, so a gather may overlap the decode of its own
+    # step and the whole next step; a step waits only for the gather of two steps back (buffer
+    # reuse).  Every gather still completes inside the timed region (the final synchronize).
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
+    sizes = [torch.empty_like(B.clen) for _ in range(2)] if world > 1 else None
+    gathered = [torch.cuda.Event() for _ in range(2)] if world > 1 else None
+    nstep = [0]
 
     def step():
         B.encode(stream)
         if world > 1:
-            # the one exchange step: sizes all-gathered over RCCL and scanned in global order, on
-            # its own stream so it overlaps the decode (which does not need the global offsets)
+            k = nstep[0] % 2
+            nstep[0] += 1
+            stream.wait_event(gathered[k])
+            sizes[k].copy_(B.clen)
             comm.wait_stream(stream)
             with torch.cuda.stream(comm):
-                shard.global_offsets(B.clen, world)
+                shard.global_offsets(sizes[k], world)
+                gathered[k].record(comm)
         B.decode(stream)
-        if world > 1:
-            stream.wait_stream(comm)   # the next encode rewrites the sizes the gather reads
 
     for _ in range(max(1, args.warmup)):
         step()
