@@ -158,8 +158,16 @@ __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
 #ifndef RLE_NOSTORE
 #define RLE_NOSTORE 0
 #endif
-__device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v) {
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+// Output stores.  wt (wave-uniform): write through (sc1: the line leaves the XCD's L2 and is not
+// kept dirty there).  A launch whose whole output fits in L2 otherwise ends with all of it dirty,
+// and the kernel boundary writes it back at about 6 TB/s (MI355X_MICROARCH.md, kernel boundaries):
+// 2.8 us for configs[1]'s 16.8 MB of decoded output.  Large launches store plainly, where writing
+// through measured 6-14 % slower (the launchers choose; rle_kernels.hip).
+__device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v, bool wt) {
+    if (wt)
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+    else
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
 // wait until at most n vector-memory ops are outstanding
 #define RLE_VMW(N)                                            \
@@ -338,6 +346,7 @@ struct EncState {
     u32 prev_top;   // input byte at tile_pos-1, in bits 24..31
     u32 rs;         // start position of the run holding input byte tile_pos-1
     u32 head;       // leading bytes of the first stored chunk that belong to the previous segment
+    bool wt;        // write-through output stores (vstore)
     Stamps sp;      // diagnostic builds only
 };
 
@@ -511,7 +520,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
         // garbage it never stores, and LDS reads do not fault
         const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16u * (c + 1u));
         const bool skip = st.head && c == 0u;   // shared with the previous segment: byte stores below
-        vstore(rso, (c < nfl && !skip && !(RLE_EABL & 4)) ? st.flushed + 16u * c : kOOB, v);
+        vstore(rso, (c < nfl && !skip && !(RLE_EABL & 4)) ? st.flushed + 16u * c : kOOB, v, st.wt);
         if (skip && nfl) {
             const u32 wv[4] = {v.x, v.y, v.z, v.w};
             for (u32 j = st.head; j < 16u; ++j) dst[st.flushed + j] = (uint8_t)(wv[j >> 2] >> (8u * (j & 3u)));
@@ -597,6 +606,7 @@ struct DecState {
     u32 tail;      // 0x100|byte when the stream ends in an unbounded-count token, else 0
     u32 head;      // leading bytes of the first stored chunk that belong to the previous segment
     u32 prev;      // stream byte before the current tile, in bits 24..31
+    bool wt;       // write-through output stores (vstore)
     Stamps sp;     // diagnostic builds only
 };
 
@@ -618,7 +628,7 @@ __device__ __forceinline__ u32 sswz(u32 t) {
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
-__device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
+__device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
                                          u32& head, uint8_t* dst, Stamps& sp) {
     const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
@@ -666,7 +676,7 @@ __device__ __forceinline__ u32 dec_flush(u32 nfl, u32 lane, uint8_t* stage, u32x
         o.w = __builtin_amdgcn_perm(L[7], L[6], 0x06040200u);
         RLE_STAMP(sp, 4);   // flush: fill + carry
         const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
-        vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o);   // RLE_NOSTORE: diagnostic
+        vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o, wt);   // RLE_NOSTORE: diagnostic
         if (skip && active) {
             const u32 wv[4] = {o.x, o.y, o.z, o.w};
             for (u32 j = head; j < 16u; ++j) dst[flushed + j] = (uint8_t)(wv[j >> 2] >> (8u * (j & 3u)));
@@ -891,7 +901,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
 
     const u32 newrel = rel0 + ttot;
     const u32 nfl = newrel >> 4;
-    const u32 rounds = dec_flush(nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
+    const u32 rounds = dec_flush(st.wt, nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
     if (nfl) {   // move the partial chunk to staging chunk 1
         if (lane < 8u) {
             auto* from = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u * (nfl + 1u) + 4u * lane));
@@ -937,7 +947,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
             if (16u * q + 16u <= span && j0 == 0u) {
                 u32x4 o;
                 o.x = ob[0]; o.y = ob[1]; o.z = ob[2]; o.w = ob[3];
-                vstore(rso, st.flushed + 16u * q, o);
+                vstore(rso, st.flushed + 16u * q, o, st.wt);
             } else {
                 for (u32 j = j0; j < 16u && 16u * q + j < span; ++j)
                     dst[st.flushed + 16u * q + j] = (uint8_t)(ob[j >> 2] >> (8u * (j & 3u)));

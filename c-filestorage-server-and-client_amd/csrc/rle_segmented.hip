@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         const u32 rs = uniform(pl.x), off = uniform(pl.y);
         const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U + U / 2u);
-        EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, {}};
+        EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, false, {}};
         const EncK kc = enc_k();
         walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
             return enc_tile(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc);
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         const u32 e = uniform(pl.x), off = uniform(pl.y);
         const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, {}};
+        DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, false, {}};
         const DecK kc = dec_k();
         const bool serial = walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
             return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc);
