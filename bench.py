@@ -128,14 +128,17 @@ class Batch:
 
 
 def time_kernels(fn, reps, stream):
-    """Average duration of fn's launch, from HIP events on the stream the kernel runs on."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in evs:
-        a.record(stream)
+    """Average duration of fn's launch: reps launches back to back on the stream the kernel runs on,
+    between one pair of HIP events (an event pair around every launch would add its own dispatch,
+    ~2 us, to each; back to back, each launch carries only its share of the kernel boundaries)."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    a.record(stream)
+    for _ in range(reps):
         fn()
-        b.record(stream)
+    b.record(stream)
     torch.cuda.synchronize()
-    return sum(a.elapsed_time(b) for a, b in evs) / reps * 1e-3
+    return a.elapsed_time(b) / reps * 1e-3
 
 
 def cpu_baseline(wl, seconds, threads, flavor):
