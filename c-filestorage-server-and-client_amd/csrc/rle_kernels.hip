@@ -277,14 +277,17 @@ inline uint32_t grid_for(uint32_t n, uint32_t waves) {
 // kWtBuffers buffers, whose output typically fits in the L2s and would otherwise all be written
 // back at the kernel boundary (configs[1], 4096 x 4 KiB: decode 15.2 -> 13.1 us, encode 14.0 ->
 // 12.6 us); plain stores above (16384 x 64 KiB: write-through 6-14 % slower).
-// RLE_MI355X_STORE=wt / wb forces one policy.
+// RLE_MI355X_STORE=wt / wb forces one policy (RLE_MI355X_STORE_ENC / _DEC: one kernel only).
 constexpr uint32_t kWtBuffers = 4096;
-uint32_t store_policy(uint32_t n) {
-    static const int force = [] {
-        const char* e = getenv("RLE_MI355X_STORE");
-        return !e ? -1 : !strcmp(e, "wt") ? 1 : !strcmp(e, "wb") ? 0 : -1;
-    }();
-    return force >= 0 ? (uint32_t)force : (n <= kWtBuffers ? 1u : 0u);
+int store_env(const char* name) {
+    const char* e = getenv(name);
+    return !e ? -1 : !strcmp(e, "wt") ? 1 : !strcmp(e, "wb") ? 0 : -1;
+}
+uint32_t store_policy(uint32_t n, bool enc) {
+    static const int force = store_env("RLE_MI355X_STORE");
+    static const int force_enc = store_env("RLE_MI355X_STORE_ENC"), force_dec = store_env("RLE_MI355X_STORE_DEC");
+    const int f = enc ? (force_enc >= 0 ? force_enc : force) : (force_dec >= 0 ? force_dec : force);
+    return f >= 0 ? (uint32_t)f : (n <= kWtBuffers ? 1u : 0u);
 }
 
 }  // namespace
@@ -299,7 +302,7 @@ extern "C" int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_of
     if (n > kMaxGrid) return RLE_E_INVAL;
     hipLaunchKernelGGL(rle::encode_kernel, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n,
-                       store_policy(n));
+                       store_policy(n, true));
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 
@@ -311,7 +314,7 @@ extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_of
     if (n > kMaxGrid) return RLE_E_INVAL;
     hipLaunchKernelGGL(rle::decode_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
-                       d_status, n, store_policy(n));
+                       d_status, n, store_policy(n, false));
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 
