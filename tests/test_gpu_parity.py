@@ -291,3 +291,22 @@ def test_decode_status_info_bits(seg):
     dec, st = gpu_decode([b"abc", b"ab\0", b"xx9" * 20000], [5, 7, 200000], seg=seg)
     assert list(st) == [R.RLE_STATUS_SHORT] * 3, st
     assert dec[0] == b"abc\0\0" and dec[1] == b"ab" + bytes(5) and dec[2] == b"x" * 180000 + bytes(20000)
+
+
+def test_large_batch_decode_plain_stores():
+    """More than 4096 buffers (plain-store launches): mixed kinds and sizes and streams the encoder
+    never emits (serial path), bit-exact against the oracle, twice in a row."""
+    rng = np.random.default_rng(21)
+    xs = [O.gen(i % 5, i, int(rng.integers(0, 6000))) for i in range(5000)]
+    ys = [O.encode(x) for x in xs]
+    streams, us, caps = list(ys), [len(x) for x in xs], [len(x) for x in xs]
+    for i in range(0, 5000, 997):   # invalid digits / counts past U, with room for the reference's writes
+        streams[i] = b"aa:" + ys[i]
+        caps[i] = us[i] + 64
+    dec, st = gpu_decode(streams, us, caps, poison=False)
+    for i in range(5000):
+        ref, _ = O.decode(streams[i], us[i], caps[i])
+        assert dec[i] == ref, i
+    assert all((st[i] & R.RLE_STATUS_SERIAL) for i in range(0, 5000, 997))
+    dec2, _ = gpu_decode(streams, us, caps, poison=False)
+    assert dec2 == dec
