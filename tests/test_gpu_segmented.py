@@ -88,3 +88,12 @@ def test_dropin_large_files_roundtrip():
         y = R.compress(x)
         assert y == O.encode(x)
         assert R.decompress(y, len(x), 5) == x + bytes(5)
+
+
+def test_dropin_very_large_file():
+    """A 192 MiB file through the drop-in: the runtime's direct copies, the segmented kernels with
+    thousands of segments, and the reference's result byte for byte."""
+    x = O.gen(2, 77, 192 << 20)
+    y = R.compress(x)
+    assert y == O.encode(x)
+    assert R.decompress(y, len(x)) == x
