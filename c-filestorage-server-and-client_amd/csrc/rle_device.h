@@ -400,8 +400,12 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
     a.B24 = B | ((from_next_lane(B, 0xFFu) & 0xFFu) << 16);   // + next 8 bytes (repeat lookahead)
 
     // run start of byte p0-1: max-scan of the last boundary position per owning lane
+    // (when every owned lane holds a boundary, each lane's own last one is already the running
+    // max: the scan is skipped -- random and 50 %-runs data nearly always; lane 63's value is then
+    // not the max, so consumers read the owned maximum from lane 62)
     const u32 lbp = (B && lane < kOwnLanes) ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
-    const u32 incl = wave_scan_incl(lbp, 0u, OpMax());
+    const bool every = (__builtin_amdgcn_ballot_w64(B == 0u) & ((1ull << kOwnLanes) - 1ull)) == 0ull;
+    const u32 incl = every ? lbp : wave_scan_incl(lbp, 0u, OpMax());
     a.incl = incl;
     const u32 pm = from_prev_lane(incl, 0u);
     const u32 rsl = pm > rs ? pm : rs;
@@ -536,7 +540,7 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
     st.prev_top = readlane(top, kOwnLanes - 1u);
-    const u32 i63 = readlane(incl, 63);
+    const u32 i63 = readlane(incl, kOwnLanes - 1u);
     st.rs = i63 > st.rs ? i63 : st.rs;
     RLE_STAMP(st.sp, 5);   // partial-chunk move, state
     return rounds;

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_
                 if (fb != kNone) fbm = fb <= an.p0 ? 0xFFFFu : (fb >= an.p0 + 16u ? 0u : ~lowmask(fb - an.p0) & 0xFFFFu);
                 rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
                 prev_top = readlane(an.top, kOwnLanes - 1u);
-                const u32 i63 = readlane(an.incl, 63);
+                const u32 i63 = readlane(an.incl, kOwnLanes - 1u);
                 rs = i63 > rs ? i63 : rs;
                 return 0u;
             });
