@@ -310,3 +310,25 @@ def test_large_batch_decode_plain_stores():
     assert all((st[i] & R.RLE_STATUS_SERIAL) for i in range(0, 5000, 997))
     dec2, _ = gpu_decode(streams, us, caps, poison=False)
     assert dec2 == dec
+
+
+@pytest.mark.parametrize("n", [4097, 4099, 8195, 12288])
+def test_decode_ragged_batches_past_one_round(n):
+    """Batches just past one residency round of the chip (4096 waves): a last round of one to a few
+    buffers, XCD-padding workgroups with no buffer, and long / short / serial buffers mixed --
+    each buffer decoded exactly once, bit-exact, every status written."""
+    rng = np.random.default_rng(n)
+    sizes = rng.integers(0, 3000, size=n)
+    sizes[::7] = 20000   # a few long buffers, so ranges finish unevenly
+    xs = [O.gen(i % 5, 7 * i + 1, int(sizes[i])) for i in range(n)]
+    streams = [O.encode(x) for x in xs]
+    us, caps = [len(x) for x in xs], [len(x) for x in xs]
+    for i in range(3, n, 1001):
+        streams[i] = b"aa:" + streams[i]
+        caps[i] = us[i] + 64
+    dec, st = gpu_decode(streams, us, caps)
+    for i in range(n):
+        ref, _ = O.decode(streams[i], us[i], caps[i])
+        assert dec[i] == ref, i
+    assert all(st[i] != 0x7777 and (st[i] & R.RLE_STATUS_SERIAL) for i in range(3, n, 1001))
+    assert all(st[i] & ~R.RLE_STATUS_SHORT == 0 for i in range(n) if (i - 3) % 1001)
