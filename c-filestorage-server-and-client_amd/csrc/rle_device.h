@@ -192,52 +192,69 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // stop).  Vector-memory ops complete in issue order, so the wait for tile t+1 (issued inside step
 // t-1, before that step's stores) leaves step t-1's stores, the refill and step t's stores in
 // flight.  Loads past the buffer (t+2 >= ntiles) are range-checked to zero and cost no traffic.
+//
+// Encode of small buffers (enc_tile<true>): tiles do not overlap.  All 64 lanes own 16 bytes (tile t
+// is [1024 t, 1024 t + 1024)), and the 16 bytes after the tile, which lane 63 looks ahead into,
+// come with a second one-lane DMA into the slot's tail (kLook).  A 4 KiB buffer is then 4 tiles
+// instead of 5; the extra work per tile (≈5 %) outweighs the saving from about 16 KiB up.
 constexpr u32 kOwnLanes = 63;
-constexpr u32 kTileStep = 16 * kOwnLanes;   // 1008
+constexpr u32 kTileStep = 16 * kOwnLanes;   // 1008: decode tiles
 constexpr u32 kSlot = 16 * kWave;           // 1024
+constexpr u32 kEncStep = 16 * kWave;        // 1024: encode tiles
+constexpr u32 kEncSlot = kSlot + 16;        // ... and their 16-byte lookahead
 struct Refill {
     u32x4 rs;
-    u32 voff;   // lane byte offset of tile t+2
-    u32 lds;    // slot LDS address
-    bool on;    // tile t+2 exists (wave-uniform)
+    u32 voff;    // lane byte offset of tile t+2
+    u32 lds;     // slot LDS address
+    bool on;     // tile t+2 exists (wave-uniform)
+    bool look;   // kLook walks: lane 0 also loads the 16 bytes after the tile into the slot's tail
     __device__ __forceinline__ void operator()() const {
-        if (on) dma_tile(rs, voff, lds);
+        if (on) {
+            dma_tile(rs, voff, lds);
+            if (look) dma_tile(rs, voff + kEncStep, lds + kSlot);
+        }
     }
 };
 // Tiles start at `start` (bytes from the buffer descriptor's base): tile t is [start + 1008 t, ...).
 // The first two tiles' loads; walk_tiles issues them itself unless the caller did (primed), e.g. to
 // overlap their latency with its own setup.
+// kStep: tile stride; kLook: encode tiles (kEncStep, slots of kEncSlot with the lookahead load).
+template <u32 kStep = kTileStep, bool kLook = false>
 __device__ __forceinline__ void walk_prime(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots) {
+    constexpr u32 kStride = kLook ? kEncSlot : kSlot;
     const u32 lo = start + 16u * lane;
-    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
+    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kStride;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
-    if (ntiles) dma_tile(rs, lo, l0);
-    if (ntiles > 1u) dma_tile(rs, kTileStep + lo, l1);
+    if (ntiles) Refill{rs, lo, l0, true, kLook && lane == 0u}();
+    if (ntiles > 1u) Refill{rs, kStep + lo, l1, true, kLook && lane == 0u}();
 }
 // Returns whether a step stopped the walk (~0u).
-template <class Step>
+template <u32 kStep = kTileStep, bool kLook = false, class Step>
 __device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots,
                                            Step step, bool primed = false) {
+    constexpr u32 kStride = kLook ? kEncSlot : kSlot;
+    constexpr u32 kLoads = kLook ? 2u : 1u;   // vector-memory ops per tile load
     const u32 lo = start + 16u * lane;
-    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kSlot;
+    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kStride;
+    const bool look = kLook && lane == 0u;
     // Only tiles that exist are loaded, so before step t the ops issued after tile t's load are
     // step t-2's stores, tile t+1's load (if t+1 < ntiles) and step t-1's stores.  Stores are never
     // waited for: nothing in the wave reads them back, and a wave may end with stores in flight.
     // Loads are all consumed by the last step, so only a walk that stops early (~0u) drains.
-    if (!primed) walk_prime(rs, start, ntiles, lane, slots);
+    if (!primed) walk_prime<kStep, kLook>(rs, start, ntiles, lane, slots);
     u32 p1 = 0, p2 = 0;   // stores of the last step and of the one before
     for (u32 t = 0; t < ntiles; t += 2) {
-        vm_wait(p2 + (t + 1u < ntiles ? 1u : 0u) + p1);
+        vm_wait(p2 + (t + 1u < ntiles ? kLoads : 0u) + p1);
         p2 = p1;
-        p1 = step(t, slots, Refill{rs, (t + 2u) * kTileStep + lo, l0, t + 2u < ntiles});
+        p1 = step(t, slots, Refill{rs, (t + 2u) * kStep + lo, l0, t + 2u < ntiles, look});
         if (p1 == ~0u) {
             vm_drain();
             return true;
         }
         if (t + 1u >= ntiles) break;
-        vm_wait(p2 + (t + 2u < ntiles ? 1u : 0u) + p1);
+        vm_wait(p2 + (t + 2u < ntiles ? kLoads : 0u) + p1);
         p2 = p1;
-        p1 = step(t + 1u, slots + kSlot, Refill{rs, (t + 3u) * kTileStep + lo, l1, t + 3u < ntiles});
+        p1 = step(t + 1u, slots + kStride, Refill{rs, (t + 3u) * kStep + lo, l1, t + 3u < ntiles, look});
         if (p1 == ~0u) {
             vm_drain();
             return true;
@@ -246,6 +263,7 @@ __device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
     return false;
 }
 __device__ __forceinline__ u32 ntiles_for(u32 n) { return (n + kTileStep - 1u) / kTileStep; }
+__device__ __forceinline__ u32 enc_ntiles_for(u32 n) { return (n + kEncStep - 1u) / kEncStep; }
 
 // packed u16 max
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -354,18 +372,25 @@ struct EncState {
 // wave owns: the buffer, or its segment); runs end at Ud (the buffer's end).
 // Analysis of one encode tile (shared by enc_tile and the segment summary): per lane, the run
 // boundary mask B (+ the next lane's 8 bits in B24), token starts T and 3-byte tokens P, and the
-// wave max-scan of the last boundary position.
+// wave max-scan of the last boundary position.  k64 (1024-byte tiles): all 64 lanes own their 16
+// bytes, and `look` holds the first 8 bytes after the tile (the slot's tail, the same for every
+// lane), from which lane 63 takes its next-lane bits.  Else lane 63 holds the next tile's first 16
+// bytes (lookahead only) and `look` is unused.
 struct EncAn {
     u32 w[4];
     u32 p0, validm, top, B, B24, incl, T, P;
 };
 // Register constants of the encode tile, made once per kernel (vconst: no rematerialisation).
 struct EncK {
-    u32 K80, C1, C2;
+    u32 K80, C1, C2, V01;
 };
-__device__ __forceinline__ EncK enc_k() { return EncK{vconst(0x80808080u), vconst(0x08040201u), vconst(0x80402010u)}; }
-__device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u32 Uo, u32 lane, u32 prev_top,
-                                             u32 rs, const EncK& kc) {
+__device__ __forceinline__ EncK enc_k() {
+    return EncK{vconst(0x80808080u), vconst(0x08040201u), vconst(0x80402010u), vconst(0x01010101u)};
+}
+template <bool k64>
+__device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, const uint2 look, u32 pos, u32 Ud, u32 Uo, u32 lane,
+                                             u32 prev_top, u32 rs, const EncK& kc) {
+    const bool owned = k64 || lane < kOwnLanes;
     EncAn a;
     a.w[0] = cur.x; a.w[1] = cur.y; a.w[2] = cur.z; a.w[3] = cur.w;
     const u32* w = a.w;
@@ -374,7 +399,7 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
     const u32 left = p0 < Ud ? Ud - p0 : 0u;
     const u32 nl = left < 16u ? left : 16u;
     const u32 lefto = p0 < Uo ? Uo - p0 : 0u;
-    const u32 validm = lane < kOwnLanes ? lowmask(lefto < 16u ? lefto : 16u) : 0u;   // lane 63: lookahead only
+    const u32 validm = owned ? lowmask(lefto < 16u ? lefto : 16u) : 0u;   // else lookahead only
     a.validm = validm;
 
     // run boundaries: bit j <=> x[p0+j] != x[p0+j-1] (or p0+j == 0); positions >= Ud end runs
@@ -397,14 +422,26 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
     B |= (p0 == 0u) ? 1u : 0u;
     B |= ~lowmask(nl) & 0xFFFFu;
     a.B = B;
-    a.B24 = B | ((from_next_lane(B, 0xFFu) & 0xFFu) << 16);   // + next 8 bytes (repeat lookahead)
+    // + the next lane's first 8 boundary bits (repeat lookahead); with k64, lane 63 compares the
+    // tile's lookahead bytes against its last byte
+    u32 Bn = 0xFFu;
+    if (k64) {
+        const u32 q0 = look.x ^ alignbyte(look.x, w[3], 3), q1 = look.y ^ alignbyte(look.y, look.x, 3);
+        const u32 gq0 = bitop3<kOrAnd>(((q0 & 0x7F7F7F7Fu) + 0x7F7F7F7Fu), q0, K80);
+        const u32 gq1 = bitop3<kOrAnd>(((q1 & 0x7F7F7F7Fu) + 0x7F7F7F7Fu), q1, K80);
+        const u32 nl2 = left > 16u ? left - 16u : 0u;
+        Bn = (__builtin_amdgcn_udot4(gq1, C2, __builtin_amdgcn_udot4(gq0, C1, 0u, false), false) >> 7) |
+             (~lowmask(nl2 < 8u ? nl2 : 8u) & 0xFFu);
+    }
+    a.B24 = B | ((from_next_lane(B, Bn) & 0xFFu) << 16);
 
     // run start of byte p0-1: max-scan of the last boundary position per owning lane
     // (when every owned lane holds a boundary, each lane's own last one is already the running
-    // max: the scan is skipped -- random and 50 %-runs data nearly always; lane 63's value is then
-    // not the max, so consumers read the owned maximum from lane 62)
-    const u32 lbp = (B && lane < kOwnLanes) ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
-    const bool every = (__builtin_amdgcn_ballot_w64(B == 0u) & ((1ull << kOwnLanes) - 1ull)) == 0ull;
+    // max: the scan is skipped -- random and 50 %-runs data nearly always; without k64, lane 63's
+    // value is then not the max, so consumers read the owned maximum from lane 62)
+    const u32 lbp = (B && owned) ? p0 + 31u - (u32)__builtin_clz(B) : 0u;
+    constexpr uint64_t kOwnedMask = k64 ? ~0ull : (1ull << kOwnLanes) - 1ull;
+    const bool every = (__builtin_amdgcn_ballot_w64(B == 0u) & kOwnedMask) == 0ull;
     const u32 incl = every ? lbp : wave_scan_incl(lbp, 0u, OpMax());
     a.incl = incl;
     const u32 pm = from_prev_lane(incl, 0u);
@@ -429,7 +466,7 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, u32 pos, u32 Ud, u
 // address of the lane's first output byte; byte i of Q = output bytes of positions >= i of the
 // dword (suffix sums by right shifts), so position i writes at endk - Q.byte_i (- 2).  kFull: all
 // 16 positions of every owned lane are valid, so the non-starts are V01 - T01 (V01 = 0x01010101 on
-// lanes 0..62, 0 on the lookahead lane) without an expansion of their own.
+// owned lanes, 0 on a lookahead lane) without an expansion of their own.
 template <bool kFull>
 __device__ __forceinline__ void enc_pass1(const u32* w, u32 T, u32 P, u32 NS, u32 e0, u32 V01) {
     u32 endk = e0;
@@ -451,13 +488,16 @@ __device__ __forceinline__ void enc_pass1(const u32* w, u32 T, u32 P, u32 NS, u3
     }
 }
 
+template <bool k64>
 __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
                                         u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
                                         const EncK& kc) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    const uint2 look = k64 ? *reinterpret_cast<const uint2*>(cslot + kSlot) : uint2{0u, 0u};
     next();   // the slot is free once read
-    const EncAn an = enc_analyze(cur, pos, Ud, Uo, lane, st.prev_top, st.rs, kc);
+    const EncAn an = enc_analyze<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, st.rs, kc);
+    constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;   // the tile's last owning lane
     const u32* w = an.w;
     const u32 validm = an.validm, top = an.top, B24 = an.B24, incl = an.incl, T = an.T, P = an.P;
 
@@ -480,7 +520,8 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     // of the dword (suffix sums by right shifts), so position i writes at endk - Q.byte_i (- 2)
     if (!(RLE_EABL & 1)) {
         const u32 e0 = lds_addr(stage) + 16u + rel0 + oincl - nout;
-        if (pos + kTileStep <= Uo) enc_pass1<true>(w, T, P, NS, e0, lane < kOwnLanes ? 0x01010101u : 0u);
+        if (pos + (k64 ? kEncStep : kTileStep) <= Uo)
+            enc_pass1<true>(w, T, P, NS, e0, (k64 || lane < kOwnLanes) ? kc.V01 : 0u);
         else enc_pass1<false>(w, T, P, NS, e0, 0u);
     }
     RLE_STAMP(st.sp, 2);   // pass 1
@@ -539,8 +580,8 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     wave_lds_sync();
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
-    st.prev_top = readlane(top, kOwnLanes - 1u);
-    const u32 i63 = readlane(incl, kOwnLanes - 1u);
+    st.prev_top = readlane(top, kLast);
+    const u32 i63 = readlane(incl, kLast);
     st.rs = i63 > st.rs ? i63 : st.rs;
     RLE_STAMP(st.sp, 5);   // partial-chunk move, state
     return rounds;

@@ -32,6 +32,10 @@ __device__ __forceinline__ u32 xcd_buffer(u32 wg, u32 ngrid, u32 waves, u32 wid)
 #define RLE_ENC_WAVES 4
 #endif
 constexpr u32 kEncWaves = RLE_ENC_WAVES;
+#ifndef RLE_ENC_SMALL   // largest buffer encoded in 1024-byte tiles
+#define RLE_ENC_SMALL 16384
+#endif
+constexpr u32 kEncSmall = RLE_ENC_SMALL;
 constexpr u32 kEncBlock = kWave * kEncWaves;
 __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
@@ -40,12 +44,12 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ out_off,
                                                            uint64_t* __restrict__ out_len,
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * 2 * kEncSlot];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kEncWaves * kEncStage];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     uint8_t* stage = stage_all + wid * kEncStage;
-    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    const uint8_t* slots = slots_all + wid * 2 * kEncSlot;
     const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kEncWaves, wid);
     if (b >= n) return;
     const uint64_t U64 = in_len[b];
@@ -69,9 +73,16 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
     st.sp.last = memtime();
 #endif
-    walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-        return enc_tile(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc);
-    });
+    // 1024-byte tiles where they save a tile, up to kEncSmall (rle_device.h, enc_tile<true>)
+    if (enc_ntiles_for(U) < ntiles_for(U) && U <= kEncSmall)
+        walk_tiles<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
+                                   [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                                       return enc_tile<true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc);
+                                   });
+    else
+        walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+            return enc_tile<false>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc);
+        });
     RLE_STAMP(st.sp, 6);   // drain
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
     if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];

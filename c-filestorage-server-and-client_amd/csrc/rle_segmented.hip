@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_
             walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
                 nx();
-                const EncAn an = enc_analyze(cur, p0 + t * kTileStep, U, p1, lane, prev_top, rs, kc);
+                const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, p0 + t * kTileStep, U, p1, lane, prev_top, rs, kc);
                 // run boundaries inside the segment: the first one (L0) and the last one (lb)
                 const u32 Bo = an.B & an.validm;
                 const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, false, {}};
         const EncK kc = enc_k();
         walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return enc_tile(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc);
+            return enc_tile<false>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc);
         });
         // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past this
         // segment's output and nothing before it

@@ -164,6 +164,27 @@ def test_ragged_sizes_and_tile_edges():
     _oracle_parity(xs)
 
 
+def test_encode_tile_forms_at_their_edges():
+    """Both encode tile forms (csrc/rle_device.h enc_tile: 1024-byte tiles for buffers up to 16 KiB
+    where they save a tile, 1008-byte overlapped tiles otherwise) at sizes around every multiple
+    of 1008 and 1024 up to 17 tiles, with runs that end, or cross a tile boundary, 1..10 bytes
+    before or after it (the lookahead bits of lane 63, the 9-byte token cut, digits '1'..'9')."""
+    xs = []
+    for k in range(1, 18):
+        for base in (1008 * k, 1024 * k):
+            for d in (-17, -9, -2, -1, 0, 1, 2, 8, 9, 16, 17):
+                n = base + d
+                xs.append(O.gen(k % 5, n, n))
+                for r in (1, 2, 3, 8, 9, 10):
+                    for side in (-1, 1):
+                        edge = 1024 * (k - 1) + (1024 if side > 0 else 1008)
+                        x = bytearray(O.gen(1, 31 * n + r, n))
+                        lo, hi = max(0, edge - r), min(n, edge + r * (side > 0))
+                        x[lo:hi] = b"7" * (hi - lo)
+                        xs.append(bytes(x))
+    _oracle_parity(xs)
+
+
 def test_long_runs_across_tiles():
     xs = [bytes(1 << 20), b"\xff" * 100000, b"a" * 9 * 1024, b"a" * (9 * 1024 + 1), b"\0" * 1023 + b"a" * 3000,
           O.gen(3, 5, 1 << 20), O.gen(4, 5, 300001), O.gen(2, 6, 777777)]
