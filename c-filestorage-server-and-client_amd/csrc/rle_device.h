@@ -32,7 +32,7 @@ typedef uint32_t u32;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr u32 kWave = 64;
-constexpr u32 kMaxBufferBytes = 0x7FFFFFF0u;   // per-buffer limit (32-bit in-buffer offsets)
+constexpr u32 kMaxBufferBytes = RLE_MAX_BUFFER_BYTES;   // per-buffer limit (32-bit in-buffer offsets)
 constexpr u32 kOOB = 0x80000000u;               // store offset dropped by the range check
 
 // ---------------------------------------------------------------- cross-lane primitives (DPP)

@@ -58,6 +58,17 @@ inline uint64_t now_ns() {
 inline void check(hipError_t e, const char* what) {
     if (e != hipSuccess) die(what, e);
 }
+// Buffers past RLE_MAX_BUFFER_BYTES (2 GiB) are not handled by the kernels: the call fails with
+// errno = EFBIG (reported once on stderr) instead of returning a wrong result.
+std::atomic<int> g_warned_big{0};
+bool too_big(const char* who, size_t n) {
+    if (n <= RLE_MAX_BUFFER_BYTES) return false;
+    if (!g_warned_big.exchange(1))
+        fprintf(stderr, "librle_mi355x: %s: %zu bytes exceeds the per-buffer limit of %u\n", who, n,
+                (unsigned)RLE_MAX_BUFFER_BYTES);
+    errno = EFBIG;
+    return true;
+}
 
 // Small-call threshold: up to this many input bytes the worst-case output is copied back in the
 // same round trip as its size (one stream sync instead of two).
@@ -506,9 +517,9 @@ bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* a
 // src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes.
 extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize) {
     const size_t U = origSize;
-    if (U == 0) {
+    if (U == 0 || too_big("RLEcompress", U)) {
         *compressedSize = 0;
-        return static_cast<char*>(calloc(16, 1));
+        return U == 0 ? static_cast<char*>(calloc(16, 1)) : nullptr;
     }
     Ctx* c = ctx();
     if (U < kSegEncodeBytes) {   // one wave walks it: the single-copy path
@@ -556,6 +567,7 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
 // src/rleCompression.c:47-62 — returns a malloc block of U+E bytes (decoded U, then E zeros).
 extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompressedSize, size_t extraAllocation) {
     const size_t C = compressedSize, U = uncompressedSize, E = extraAllocation, total = U + E;
+    if (too_big("RLEdecompress", C) || too_big("RLEdecompress", U)) return nullptr;
     char* r = static_cast<char*>(malloc(total ? total : 1));
     if (!r) return nullptr;
     if (C == 0) {  // nothing to decode: calloc'd block (:48)
@@ -614,6 +626,10 @@ extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompresse
     // U == 0: the decode keeps nothing below U and whatever it writes into the extra region is
     // overwritten by the appended bytes (:767-770), so the result is encode(newContent)
     if (U == 0) return RLEcompress(const_cast<char*>(newContent), A, newCompressedSize);
+    if (too_big("RLEappend", C) || too_big("RLEappend", U + A)) {
+        *newCompressedSize = 0;
+        return nullptr;
+    }
     Ctx* c = ctx();
     if (C && C < kSegDecodeBytes && 16 + A < kSegEncodeBytes &&
         rle_max_compressed_size(16 + A) <= kOneTripBytes) {
@@ -725,6 +741,7 @@ extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compres
             errno = EINVAL;
             return -1;
         }
+        if (too_big("RLEdecompressN", C) || too_big("RLEdecompressN", U)) return -1;
         idx.push_back(i);
         inTot += round16(C);
         outTot += round16(U);

@@ -10,7 +10,8 @@
  *        memcpy(d + uncompressedSize, newContent, newContentLen);
  *        out = RLEcompress(d, uncompressedSize + newContentLen, &newCompressedSize); free(d);
  *    in one device round trip.  Returns what `out` would be (a malloc block: C' token bytes plus
- *    at least 2 zero bytes; *newCompressedSize = C'), NULL only on allocation failure.  The old
+ *    at least 2 zero bytes; *newCompressedSize = C'), NULL only on allocation failure or, with
+ *    errno = EFBIG, for content past RLE_MAX_BUFFER_BYTES (2 GiB).  The old
  *    stream's tokens before its final one are kept and only c^r ‖ newContent is re-encoded (r <= 9,
  *    rle_mi355x.h rle_append_prepare_device), which equals the reference result whenever `content`
  *    is encoder output — the only content the server stores (filesystemApi.c:774 -> :812; a new
@@ -23,7 +24,7 @@
  *    RLEdecompress(data[i], compressedSize[i], uncompressedSize[i], 0) written into the caller's
  *    buffer out[i] (uncompressedSize[i] bytes; readNFiles can pass its response buffer at the
  *    file's offset and skip the per-file malloc/memcpy/free).  Returns 0, or -1 with errno =
- *    EINVAL (a NULL array) / ENOMEM.
+ *    EINVAL (a NULL array) / ENOMEM / EFBIG (a file past RLE_MAX_BUFFER_BYTES, 2 GiB).
  */
 #ifndef RLE_FILEOPS_H
 #define RLE_FILEOPS_H

@@ -39,11 +39,14 @@ extern "C" {
 #define RLE_E_HIP      (-2)   /* a HIP runtime call failed */
 #define RLE_E_NODEV    (-3)   /* no usable gfx950 device */
 
+/* Largest buffer (input or decoded) one kernel handles: in-buffer offsets are 32-bit. */
+#define RLE_MAX_BUFFER_BYTES 0x7FFFFFF0u
+
 /* per-buffer status bits (d_status[i]) */
 #define RLE_STATUS_OK          0u
 #define RLE_STATUS_OVERFLOW    1u      /* decode: stream writes past cap (reference: heap overflow); truncated */
 #define RLE_STATUS_MISALIGNED  2u      /* input or output slot not 16-byte aligned; buffer skipped */
-#define RLE_STATUS_TOOLARGE    4u      /* buffer larger than 0x7FFFFFF0 bytes (2 GiB); buffer skipped */
+#define RLE_STATUS_TOOLARGE    4u      /* buffer larger than RLE_MAX_BUFFER_BYTES (2 GiB); buffer skipped */
 #define RLE_STATUS_SERIAL      0x100u  /* info: stream decoded by the exact serial path (not encoder output) */
 #define RLE_STATUS_SHORT       0x400u  /* info: the stream decodes to fewer than U bytes, the rest is zero
                                           (not encoder output) */

@@ -2,6 +2,7 @@
 headers in include/ declare; the drop-in header is plain C99 (as the reference's callers compile
 it, Makefile:6) and declares the reference prototypes (include/rleCompression.h:4-5)."""
 import ctypes
+import errno
 import os
 import re
 import subprocess
@@ -44,6 +45,40 @@ def test_host_only_entry_points():
     assert R.max_compressed_size(4096) == 6144
     assert "gfx950" in R.version()
     assert R.device_count() >= 0
+
+
+def test_oversized_buffers_fail_with_efbig():
+    """Past RLE_MAX_BUFFER_BYTES (include/rle_mi355x.h) every drop-in entry fails explicitly
+    (NULL / -1, errno EFBIG) before touching the data or the GPU -- never a wrong result."""
+    L = ctypes.CDLL(R.lib()._name, use_errno=True)
+    big = 0x7FFFFFF0 + 1
+    buf = ctypes.create_string_buffer(64)
+    c = ctypes.c_size_t(123)
+    L.RLEcompress.restype = ctypes.c_void_p
+    L.RLEcompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    ctypes.set_errno(0)
+    assert L.RLEcompress(buf, big, ctypes.byref(c)) is None
+    assert ctypes.get_errno() == errno.EFBIG and c.value == 0
+    L.RLEdecompress.restype = ctypes.c_void_p
+    L.RLEdecompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
+    for C, U in ((big, 16), (16, big)):
+        ctypes.set_errno(0)
+        assert L.RLEdecompress(buf, C, U, 0) is None
+        assert ctypes.get_errno() == errno.EFBIG
+    L.RLEappend.restype = ctypes.c_void_p
+    L.RLEappend.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                            ctypes.POINTER(ctypes.c_size_t)]
+    ctypes.set_errno(0)
+    c.value = 5
+    assert L.RLEappend(buf, 3, big - 1, buf, 2, ctypes.byref(c)) is None
+    assert ctypes.get_errno() == errno.EFBIG and c.value == 0
+    L.RLEdecompressN.restype = ctypes.c_int
+    L.RLEdecompressN.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                 ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_char_p)]
+    ptrs = (ctypes.c_char_p * 1)(ctypes.cast(buf, ctypes.c_char_p))
+    ctypes.set_errno(0)
+    assert L.RLEdecompressN(1, ptrs, (ctypes.c_size_t * 1)(big), (ctypes.c_size_t * 1)(16), ptrs) == -1
+    assert ctypes.get_errno() == errno.EFBIG
 
 
 def test_reference_prototypes_exact():
