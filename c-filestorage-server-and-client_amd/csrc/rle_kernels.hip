@@ -107,6 +107,105 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
 // so short (highly compressed) and long buffers balance without a software queue.
 constexpr u32 kDecWaves = RLE_DEC_WAVES;
 constexpr u32 kDecBlock = kWave * kDecWaves;
+// Issue order of a large decode batch (longest first): buffer indices sorted by descending tile
+// count, a counting sort over kOrderBuckets clamped keys (order inside a bucket is arbitrary).
+// Heavy buffers then start in the first residency round, and the four waves of a workgroup,
+// which hold its LDS until the last one ends, get buffers of similar cost.  Outputs do not depend
+// on the order.  Two small launches, histogram and scatter, over hist[] and cursor[] (both zeroed
+// by the launcher).
+constexpr u32 kOrderBuckets = 2048;
+__device__ __forceinline__ u32 order_key(uint64_t C) {
+    const uint64_t t = (C + kTileStep - 1u) / kTileStep;
+    return t < kOrderBuckets - 1u ? (u32)t : kOrderBuckets - 1u;
+}
+// The lanes of a wave that share a key make one atomic: per distinct key, the first such lane adds
+// the group's size, and each lane's place is the group's base plus its rank in the group (a
+// uniform batch: one atomic per wave).  All 64 lanes call it; `on` marks the lanes with an item.
+__device__ __forceinline__ u32 grouped_add(u32* hist, u32 key, bool on, u32 lane) {
+    const uint64_t lt = (1ull << lane) - 1ull;
+    u32 pos = 0u;
+    uint64_t todo = __builtin_amdgcn_ballot_w64(on);
+    while (todo) {
+        const u32 lead = (u32)__builtin_ctzll(todo);
+        const u32 kl = readlane(key, lead);
+        const uint64_t grp = __builtin_amdgcn_ballot_w64(on && key == kl);
+        u32 base = 0u;
+        if (lane == lead) base = atomicAdd(&hist[kl], (u32)__builtin_popcountll(grp));
+        base = readlane(base, lead);
+        if ((grp >> lane) & 1ull) pos = base + (u32)__builtin_popcountll(grp & lt);
+        todo &= ~grp;
+    }
+    return pos;
+}
+// Each workgroup takes kOrderChunk consecutive buffers (kOrderPer per thread), counts them in an
+// LDS histogram and adds its non-empty buckets to the global one: one global atomic per bucket and
+// workgroup.
+constexpr u32 kOrderPer = 4;
+constexpr u32 kOrderChunk = 256u * kOrderPer;
+__device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kOrderPer],
+                                            u32 (&rank)[kOrderPer]) {
+    const u32 t = threadIdx.x, lane = t & (kWave - 1);
+    for (u32 k = t; k < kOrderBuckets; k += 256u) lh[k] = 0u;
+    __syncthreads();
+    const u32 i0 = blockIdx.x * kOrderChunk + t;
+#pragma unroll
+    for (u32 j = 0; j < kOrderPer; ++j) {
+        const u32 i = i0 + 256u * j;
+        key[j] = i < n ? order_key(in_len[i]) : 0u;
+    }
+#pragma unroll
+    for (u32 j = 0; j < kOrderPer; ++j) rank[j] = grouped_add(lh, key[j], i0 + 256u * j < n, lane);
+    __syncthreads();
+}
+__global__ __launch_bounds__(256) void dec_order_hist_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
+                                                             uint32_t* __restrict__ hist) {
+    __shared__ u32 lh[kOrderBuckets];
+    u32 key[kOrderPer], rank[kOrderPer];
+    order_local(in_len, n, lh, key, rank);
+    for (u32 k = threadIdx.x; k < kOrderBuckets; k += 256u)
+        if (lh[k]) atomicAdd(&hist[k], lh[k]);
+}
+// The same local counts again.  Every workgroup scans the global counts into descending bucket
+// starts (thread t: the 8 buckets from B-1-8t down), each non-empty bucket of the workgroup takes
+// its range inside the bucket with one atomic on cursor[], and each buffer's place is bucket
+// start + range base + its rank inside the workgroup.
+__global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                const uint32_t* __restrict__ hist,
+                                                                uint32_t* __restrict__ cursor,
+                                                                uint32_t* __restrict__ order) {
+    __shared__ u32 lh[kOrderBuckets];
+    __shared__ u32 start[kOrderBuckets];
+    __shared__ u32 wsum[4];
+    constexpr u32 kPerT = kOrderBuckets / 256u;
+    const u32 t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+    u32 c[kPerT], sum = 0u;
+#pragma unroll
+    for (u32 j = 0; j < kPerT; ++j) {
+        c[j] = hist[kOrderBuckets - 1u - (kPerT * t + j)];
+        sum += c[j];
+    }
+    const u32 incl = wave_scan_incl(sum, 0u, OpAdd());
+    if (lane == kWave - 1) wsum[wv] = incl;
+    u32 key[kOrderPer], rank[kOrderPer];
+    order_local(in_len, n, lh, key, rank);   // (its barriers also publish wsum)
+    u32 base = incl - sum;
+    for (u32 w = 0; w < wv; ++w) base += wsum[w];
+#pragma unroll
+    for (u32 j = 0; j < kPerT; ++j) {
+        start[kOrderBuckets - 1u - (kPerT * t + j)] = base;
+        base += c[j];
+    }
+    for (u32 k = t; k < kOrderBuckets; k += 256u)
+        if (lh[k]) lh[k] = atomicAdd(&cursor[k], lh[k]);
+    __syncthreads();
+    const u32 i0 = blockIdx.x * kOrderChunk + threadIdx.x;
+#pragma unroll
+    for (u32 j = 0; j < kOrderPer; ++j) {
+        const u32 i = i0 + 256u * j;
+        if (i < n) order[start[key[j]] + lh[key[j]] + rank[j]] = i;
+    }
+}
+
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
                                                            const uint64_t* __restrict__ in_len,
@@ -114,7 +213,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ out_off,
                                                            const uint64_t* __restrict__ out_len,
                                                            const uint64_t* __restrict__ out_cap,
-                                                           uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+                                                           uint32_t* __restrict__ status, uint32_t n, uint32_t wt,
+                                                           const uint32_t* __restrict__ order) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kDecStage];
     __shared__ DecEntry tbl[256];
@@ -132,7 +232,15 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     DecEntry te[kTblPer];
 #pragma unroll
     for (u32 i = 0; i < kTblPer; ++i) te[i] = dec_entry_from(kDecTable.e[(threadIdx.x + i * kDecBlock) & 255u]);
-    const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
+    // with an issue order, workgroups take its ranks in dispatch order (the heavy buffers first,
+    // spread over every XCD); else each XCD takes a contiguous slice of the batch
+    u32 b;
+    if (order) {
+        const u32 slot = blockIdx.x * kDecWaves + wid;
+        b = slot < n ? uniform(order[slot]) : n;
+    } else {
+        b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
+    }
     // all five per-buffer words are loaded at once, unconditionally (index clamped; n >= 1)
     const u32 bi = b < n ? b : 0u;
     const uint64_t* capp = out_cap ? out_cap : out_len;
@@ -301,6 +409,14 @@ uint32_t store_policy(uint32_t n, bool enc) {
     return f >= 0 ? (uint32_t)f : (n <= kWtBuffers ? 1u : 0u);
 }
 
+// Decode batches past one residency round of the chip (4 workgroups of 4 waves per CU) are
+// issued longest first; RLE_MI355X_DEC_ORDER=0 turns that off.
+constexpr uint32_t kDecRound = 4096;
+bool dec_order_enabled() {
+    static const bool on = !(getenv("RLE_MI355X_DEC_ORDER") && !strcmp(getenv("RLE_MI355X_DEC_ORDER"), "0"));
+    return on;
+}
+
 }  // namespace
 
 extern "C" size_t rle_max_compressed_size(size_t U) { return U + U / 2; }
@@ -323,9 +439,26 @@ extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_of
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
-    hipLaunchKernelGGL(rle::decode_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, (hipStream_t)stream,
+    const hipStream_t s = (hipStream_t)stream;
+    // more buffers than one residency round: issue them longest first (rle::dec_order_kernel)
+    uint32_t* order = nullptr;   // [n] issue order, then [kOrderBuckets] counts and cursors
+    if (n > kDecRound && dec_order_enabled() &&
+        hipMallocAsync((void**)&order, sizeof(uint32_t) * ((size_t)n + 2u * rle::kOrderBuckets), s) != hipSuccess) {
+        (void)hipGetLastError();
+        order = nullptr;
+    }
+    if (order) {
+        uint32_t* hist = order + n;
+        uint32_t* cursor = hist + rle::kOrderBuckets;
+        const dim3 g((n + rle::kOrderChunk - 1u) / rle::kOrderChunk);
+        if (hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2u * rle::kOrderBuckets, s) != hipSuccess) return RLE_E_HIP;
+        hipLaunchKernelGGL(rle::dec_order_hist_kernel, g, dim3(256), 0, s, d_in_len, n, hist);
+        hipLaunchKernelGGL(rle::dec_order_scatter_kernel, g, dim3(256), 0, s, d_in_len, n, hist, cursor, order);
+    }
+    hipLaunchKernelGGL(rle::decode_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
-                       d_status, n, store_policy(n, false));
+                       d_status, n, store_policy(n, false), (const uint32_t*)order);
+    if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 
