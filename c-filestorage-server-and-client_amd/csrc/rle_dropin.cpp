@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <vector>
@@ -753,6 +754,15 @@ extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compres
         errno = EINVAL;
         return -1;
     }
+    // files from kSegDecodeBytes up go to the segmented form, the rest to the one-wave kernel: the
+    // large ones are packed first so that each launch takes a contiguous part of the metadata
+    const size_t mL = maxC >= kSegDecodeBytes
+                          ? (size_t)(std::stable_partition(idx.begin(), idx.end(),
+                                                           [&](size_t i) { return compressedSize[i] >= kSegDecodeBytes; }) -
+                                     idx.begin())
+                          : 0;
+    size_t inLarge = 0;
+    for (size_t k = 0; k < mL; ++k) inLarge += round16(compressedSize[idx[k]]);
     Ctx* c = ctx();
     // per-file metadata, one pinned block: in_off, in_len, out_off, out_len (m u64 each), status (m u32)
     const size_t metaBytes = 32 * m + 4 * m;
@@ -777,13 +787,15 @@ extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compres
     uint32_t* d_status = reinterpret_cast<uint32_t*>(db + 4 * m);
     check(hipMemcpyAsync(c->d_in, c->h_in, inTot, hipMemcpyHostToDevice, c->s), "H2D");
     check(hipMemcpyAsync(db, hb, 32 * m, hipMemcpyHostToDevice, c->s), "H2D(meta)");
-    if (maxC >= kSegDecodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes((uint32_t)m, inTot));
-    const int drc = maxC >= kSegDecodeBytes
-                        ? rle_decode_batch_device_seg(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr,
-                                                      d_status, (uint32_t)m, inTot, c->d_ws, c->d_ws_cap, c->s)
-                        : rle_decode_batch_device(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr,
-                                                  d_status, (uint32_t)m, c->s);
-    if (drc != RLE_OK) die("decode launch", hipGetLastError());
+    if (mL) {
+        grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes((uint32_t)mL, inLarge));
+        if (rle_decode_batch_device_seg(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr, d_status,
+                                        (uint32_t)mL, inLarge, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
+            die("decode launch", hipGetLastError());
+    }
+    if (m > mL && rle_decode_batch_device(c->d_in, db + mL, db + m + mL, c->d_out, db + 2 * m + mL, db + 3 * m + mL,
+                                          nullptr, d_status + mL, (uint32_t)(m - mL), c->s) != RLE_OK)
+        die("decode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_out, c->d_out, outTot, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipMemcpyAsync(hb + 4 * m, d_status, 4 * m, hipMemcpyDeviceToHost, c->s), "D2H(status)");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");

@@ -138,14 +138,16 @@ def fileops(seconds):
             row["reference_cpu_us"] = t_r * 1e6
         out["append"].append(row)
         print(f"append {kind} {U} done", file=sys.stderr, flush=True)
-    for n, U in ((64, 4096), (256, 4096), (64, 65536), (16, 1 << 20)):
-        xs = [gen(("random", "zero", "runs")[i % 3], U, i) for i in range(n)]
+    # uniform batches, then a mixed one: 255 small files and one of 1 MiB (segmented + one-wave)
+    for n, U in ((64, 4096), (256, 4096), (64, 65536), (16, 1 << 20), (256, None)):
+        Us = [U] * n if U else [4096] * (n - 1) + [1 << 20]
+        xs = [gen(("random", "zero", "runs")[i % 3], Us[i], i) for i in range(n)]
         ys = [R.compress(x) for x in xs]
-        bufs = [ctypes.create_string_buffer(U) for _ in range(n)]
+        bufs = [ctypes.create_string_buffer(Us[k]) for k in range(n)]
         keep = [ctypes.create_string_buffer(y, len(y) + 3) for y in ys]
         data = (ctypes.c_void_p * n)(*[ctypes.addressof(k) for k in keep])
         cs = (ctypes.c_size_t * n)(*[len(y) for y in ys])
-        us = (ctypes.c_size_t * n)(*([U] * n))
+        us = (ctypes.c_size_t * n)(*Us)
         op = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
 
         def batched():
@@ -153,14 +155,15 @@ def fileops(seconds):
 
         def looped():
             for k in range(n):
-                p = L.RLEdecompress(keep[k], cs[k], U, 0)
-                ctypes.memmove(bufs[k], p, U)
+                p = L.RLEdecompress(keep[k], cs[k], Us[k], 0)
+                ctypes.memmove(bufs[k], p, Us[k])
                 R._libc.free(p)
         t_b = _timeit(batched, seconds)
         t_l = _timeit(looped, seconds)
         assert all(bufs[k].raw == xs[k] for k in range(n))
-        out["readN"].append({"files": n, "U": U, "batched_us": t_b * 1e6, "looped_us": t_l * 1e6,
-                             "batched_GBps": n * U / t_b / 1e9, "looped_GBps": n * U / t_l / 1e9})
+        tot = sum(Us)
+        out["readN"].append({"files": n, "U": U or "255 x 4 KiB + 1 MiB", "batched_us": t_b * 1e6,
+                             "looped_us": t_l * 1e6, "batched_GBps": tot / t_b / 1e9, "looped_GBps": tot / t_l / 1e9})
         print(f"readN {n}x{U} done", file=sys.stderr, flush=True)
     return out
 
