@@ -636,11 +636,14 @@ __device__ __forceinline__ DecEntry lds_entry(u32 a) {
 // path declines count digit '1'), so no position needs a trash slot or a select.  A token decodes
 // to at most 9 bytes, so every 16-byte chunk holds a key, and the byte entering a chunk is the
 // last key of the chunk before it.
-#ifndef RLE_DEC_CHUNKS   // (smaller values: occupancy experiments on random data only)
+#ifndef RLE_DEC_CHUNKS   // staging chunks per wave; fewer: more waves per SIMD, tiles staged in passes
 #define RLE_DEC_CHUNKS 192
 #endif
 constexpr u32 kDecChunks = RLE_DEC_CHUNKS;   // >= ceil((16 + 15 + 3024 + 1) / 16): a tile decodes to <= 3024 B
 constexpr u32 kDecStage = 32u * kDecChunks;  // bytes per wave
+constexpr bool kDecOnePass = kDecChunks >= 191u;   // a whole tile's output always fits
+constexpr u32 kDecPassCap = 16u * kDecChunks - 17u;   // staged positions rel + pass may reach (rel < 16)
+static_assert(kDecChunks >= 16u, "a pass must hold at least one lane's output (144 B) past rel < 16");
 constexpr u32 kKeyFlag = 0x8000u;
 
 struct DecState {
@@ -916,47 +919,66 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     }
 
     RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
-    const u32 rel0 = st.out_pos - st.flushed;
-    // staging byte address after this lane's output (2 B per decoded position)
-    u32 endk = lds_addr(stage) + 2u * (16u + rel0 + oincl - ln.nout);
-    if (lane < kOwnLanes && !(RLE_ABL & 2)) {
-#pragma unroll
-        for (u32 k = 0; k < 4; ++k) {
-            // u16 per position: the byte, with the start flag (0x80) as the high byte: 0x80vv at a
-            // token start, an unflagged 0x00vv (ignored by the fill) anywhere else
-            const u32 xk_lo = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x05010400u);
-            const u32 xk_hi = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x07030602u);
-            u32 Q = fadd(ln.W[k], fshr<8>(ln.W[k]));
-            Q = fadd(Q, fshr<16>(Q));                        // byte i: decoded bytes of positions >= i
-            Q = Q << 1;                                      // 2 staging bytes per position
-            endk = fadd(endk, fandi<0xFFu>(Q));              // staging address after the dword's output
-            const u32 R = fadd(Q, ln.N02[k]);                // interior positions: one slot further back
-            auto put = [](u32 t, u32 key) {
-                if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
-                else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
-            };
-            put(sub_byte<0>(endk, R), xk_lo);
-            put(sub_byte<1>(endk, R), xk_lo >> 16);
-            put(sub_byte<2>(endk, R), xk_hi);
-            put(sub_byte<3>(endk, R), xk_hi >> 16);
+    // With the full staging (kDecChunks >= 191) a tile is one pass.  Smaller staging (more waves per
+    // SIMD) stages and flushes a tile in passes over consecutive lanes, each as much as fits: a pass
+    // boundary is a lane boundary, so it is a token boundary in the output, exactly like a tile
+    // boundary (runs never cross it; interior positions of a token begun in the last pass write
+    // one slot back, into a slot that holds no key).
+    u32 rounds = 0, done = 0, from = 0;
+    for (;;) {
+        const u32 rel0 = st.out_pos + done - st.flushed;
+        u32 upto = kOwnLanes, pass = ttot - done;
+        if (!kDecOnePass && rel0 + pass > kDecPassCap) {
+            // lanes whose output ends within the staging; a prefix, since oincl is monotonic, and it
+            // reaches past `from` (a lane decodes at most 144 bytes, rel0 < 16)
+            const uint64_t fit = __builtin_amdgcn_ballot_w64(oincl <= done + kDecPassCap - rel0) & kOwned;
+            upto = (u32)__builtin_popcountll(fit);
+            pass = readlane(oincl, upto - 1u) - done;
         }
-    }
-    wave_lds_sync();
-    RLE_STAMP(st.sp, 2);   // scatter
-
-    const u32 newrel = rel0 + ttot;
-    const u32 nfl = newrel >> 4;
-    const u32 rounds = dec_flush(st.wt, nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
-    if (nfl) {   // move the partial chunk to staging chunk 1
-        if (lane < 8u) {
-            auto* from = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u * (nfl + 1u) + 4u * lane));
-            auto* to = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane));
-            *to = *from;
-            *from = 0u;
+        // staging byte address after this lane's output (2 B per decoded position)
+        u32 endk = lds_addr(stage) + 2u * (16u + rel0 + oincl - done - ln.nout);
+        if (lane < upto && lane >= from && !(RLE_ABL & 2)) {
+#pragma unroll
+            for (u32 k = 0; k < 4; ++k) {
+                // u16 per position: the byte, with the start flag (0x80) as the high byte: 0x80vv at a
+                // token start, an unflagged 0x00vv (ignored by the fill) anywhere else
+                const u32 xk_lo = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x05010400u);
+                const u32 xk_hi = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x07030602u);
+                u32 Q = fadd(ln.W[k], fshr<8>(ln.W[k]));
+                Q = fadd(Q, fshr<16>(Q));                        // byte i: decoded bytes of positions >= i
+                Q = Q << 1;                                      // 2 staging bytes per position
+                endk = fadd(endk, fandi<0xFFu>(Q));              // staging address after the dword's output
+                const u32 R = fadd(Q, ln.N02[k]);                // interior positions: one slot further back
+                auto put = [](u32 t, u32 key) {
+                    if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
+                    else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
+                };
+                put(sub_byte<0>(endk, R), xk_lo);
+                put(sub_byte<1>(endk, R), xk_lo >> 16);
+                put(sub_byte<2>(endk, R), xk_hi);
+                put(sub_byte<3>(endk, R), xk_hi >> 16);
+            }
         }
         wave_lds_sync();
+        RLE_STAMP(st.sp, 2);   // scatter
+
+        const u32 newrel = rel0 + pass;
+        const u32 nfl = newrel >> 4;
+        rounds += dec_flush(st.wt, nfl, lane, stage, rso, st.flushed, st.fillc, st.head, dst, st.sp);
+        if (nfl) {   // move the partial chunk to staging chunk 1
+            if (lane < 8u) {
+                auto* from4 = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u * (nfl + 1u) + 4u * lane));
+                auto* to4 = reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane));
+                *to4 = *from4;
+                *from4 = 0u;
+            }
+            wave_lds_sync();
+        }
+        st.flushed += 16u * nfl;
+        done += pass;
+        from = upto;
+        if (upto >= kOwnLanes) break;
     }
-    st.flushed += 16u * nfl;
     st.out_pos += ttot;
     st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
     st.prev = readlane(w[3], kOwnLanes - 1u);
