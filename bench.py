@@ -259,8 +259,11 @@ def main():
     t_enc = time_kernels(lambda: B.encode(stream), reps, stream)
     t_dec = time_kernels(lambda: B.decode(stream), reps, stream)
     alg = u_local + c_bytes
-    kern = {"encode": {"us": t_enc * 1e6, "GBps": alg / t_enc / 1e9},
-            "decode": {"us": t_dec * 1e6, "GBps": alg / t_dec / 1e9}}
+    # GBps: algorithmic bytes (U + C) per second, the roofline numerator; U_GiBps: uncompressed bytes
+    # per second (SURVEY.md 8(d) reports both), also for the round trip
+    kern = {"encode": {"us": t_enc * 1e6, "GBps": alg / t_enc / 1e9, "U_GiBps": u_local / t_enc / GIB},
+            "decode": {"us": t_dec * 1e6, "GBps": alg / t_dec / 1e9, "U_GiBps": u_local / t_dec / GIB},
+            "roundtrip": {"us": (t_enc + t_dec) * 1e6, "U_GiBps": u_local / (t_enc + t_dec) / GIB}}
     dom = "encode" if t_enc >= t_dec else "decode"
     pmc = load_pmc(args.workload)
     traffic = pmc.get(dom) if isinstance(pmc, dict) else None
@@ -282,6 +285,7 @@ def main():
         nalg = N.u_bytes + nc
         ncopy = copy_ceiling(N, nalg, 20, stream)
         north = {"workload": WORKLOADS["dec64k"]["desc"], "decode_us": td * 1e6,
+                 "decode_U_GiBps": N.u_bytes / td / GIB, "encode_U_GiBps": N.u_bytes / te / GIB,
                  "decode_GBps": nalg / td / 1e9, "decode_frac": round(nalg / td / 1e9 / HBM_PEAK_GBPS, 4),
                  "encode_GBps": nalg / te / 1e9, "u_bytes": N.u_bytes, "c_bytes": nc, "verified": nok,
                  "copy_ceiling": ncopy}
