@@ -101,9 +101,11 @@ class Batch:
         self.coffs = i64(coffs)
         self.clen = torch.zeros(n, dtype=torch.int64, device=dev)
         self.status = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.d_in = torch.empty(total, dtype=torch.uint8, device=dev)
+        # zero-filled, so the padding between buffers (sizes not a multiple of 16, RLE_BENCH_PAD) is
+        # equal in d_in and d_out and the whole-arena comparison checks only the decoded bytes
+        self.d_in = torch.zeros(total, dtype=torch.uint8, device=dev)
         self.d_c = torch.empty(ctotal, dtype=torch.uint8, device=dev)
-        self.d_out = torch.empty(total, dtype=torch.uint8, device=dev)
+        self.d_out = torch.zeros(total, dtype=torch.uint8, device=dev)
         kind_t = torch.tensor([kinds[k % len(kinds)] for k in range(n)], dtype=torch.int32, device=dev)
         R.gen_synthetic(self.d_in, self.offs, self.lens, kind_t, i64(gidx))
         torch.cuda.synchronize()

@@ -683,8 +683,13 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
         const u32 c = k * kWave + lane;
         const bool active = c < nfl;
         u32x4* s4 = reinterpret_cast<u32x4*>(stage + 32u * (c + 1u));
-        // read unconditionally: an inactive lane's chunk (at most one past this wave's staging)
-        // is garbage it never stores, and LDS reads do not fault
+        // read unconditionally: an inactive lane's chunk is garbage it never stores.  With the
+        // one-pass staging (192 chunks) it lies at most one chunk past this wave's staging; with
+        // RLE_DEC_CHUNKS < 191 it can lie up to 64 * rounds - nfl chunks past it, in another wave's
+        // staging or past the workgroup's LDS.  LDS reads do not fault (out-of-range reads return
+        // 0), and from_prev_lane below hands the lane's value only to lanes that are inactive too
+        // (a lane's carry comes from the lane before it, and the active lanes are 0..nfl-1), so no
+        // stored byte depends on it.
         u32x4 a, b;
         if (RLE_SWZ == 1) {
             const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <new>
 #include <vector>
 
 #include "rleCompression.h"
@@ -98,6 +99,12 @@ constexpr int kPipeEvents = 16;
 bool g_zerocopy = true;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 
+// Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
+// staged input (and output) bytes, and a file larger than that is copied straight from / to the
+// caller's memory, so a readN of the whole store does not pin the store's size per worker thread.
+// RLE_MI355X_STAGE_CAP=<bytes> overrides it (tests use small caps to cover the chunking).
+size_t g_stage_cap = 32u << 20;
+
 struct Ctx {
     int dev = 0;
     uint8_t* h_zc = nullptr;                         // mapped pinned buffer of the zero-copy calls
@@ -168,6 +175,10 @@ void init_once() {
         if (!strcmp(e, "pinned")) g_staging = Staging::Pinned;
         else if (!strcmp(e, "pipe")) g_staging = Staging::Pipe;
     }
+    if (const char* e = getenv("RLE_MI355X_STAGE_CAP")) {
+        const long long v = atoll(e);
+        if (v >= 16) g_stage_cap = (size_t)v;
+    }
     pthread_key_create(&g_key, free_ctx);
     atexit(on_exit_handler);   // registered after the HIP runtime's own exit hooks: runs before them
 }
@@ -189,28 +200,59 @@ Ctx* ctx() {
     c->dev = (g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev);
     check(hipSetDevice(c->dev), "hipSetDevice");
     check(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking), "hipStreamCreate");
-    check(hipMalloc(&c->d_meta, kMetaSlots * sizeof(uint64_t)), "hipMalloc(meta)");
-    check(hipHostMalloc(&c->h_meta, kMetaSlots * sizeof(uint64_t), hipHostMallocDefault), "hipHostMalloc(meta)");
+    if (hipMalloc(&c->d_meta, kMetaSlots * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc(&c->h_meta, kMetaSlots * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(c->d_meta);
+        (void)hipStreamDestroy(c->s);
+        delete c;
+        throw std::bad_alloc();
+    }
     pthread_setspecific(g_key, c);
     return c;
 }
 
+// After an allocation failure part of a call may still be queued on the thread's stream: let it
+// finish before the next call reuses (or regrows) the buffers it refers to.
+void drain_after_oom() {
+    if (Ctx* c = static_cast<Ctx*>(pthread_getspecific(g_key))) (void)hipStreamSynchronize(c->s);
+    errno = ENOMEM;
+}
+
+// Staging and device buffers grow on demand (never below 16 bytes, so a launch never sees NULL).
+// A failed allocation throws std::bad_alloc, which each entry point turns into the reference's
+// allocation-failure result (NULL, or -1 with errno = ENOMEM) instead of aborting the server.
 void grow_host(uint8_t*& p, size_t& cap, size_t need) {
+    need = std::max<size_t>(need, 16);
     if (need <= cap) return;
     size_t n = cap ? cap : (64u << 10);
     while (n < need) n *= 2;
     if (p) check(hipHostFree(p), "hipHostFree");
-    check(hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault), "hipHostMalloc");
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        throw std::bad_alloc();
+    }
     cap = n;
 }
 void grow_dev(uint8_t*& p, size_t& cap, size_t need) {
+    need = std::max<size_t>(need, 16);
     if (need <= cap) return;
     size_t n = cap ? cap : (64u << 10);
     while (n < need) n *= 2;
     if (p) check(hipFree(p), "hipFree");
-    check(hipMalloc(reinterpret_cast<void**>(&p), n), "hipMalloc");
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&p), n) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        throw std::bad_alloc();
+    }
     cap = n;
 }
+
 
 }  // namespace
 
@@ -298,6 +340,9 @@ size_t pipe_chunk(size_t n) {
     return ch;
 }
 
+// Whether to_device copies n bytes through the pinned staging (else straight from the caller).
+bool staged(size_t n) { return n > 0 && !(g_staging == Staging::Direct && n >= kPipeMinBytes); }
+
 // Queues the copy of n caller bytes at src to d_dst on c->s, staged (when staged) at h_in + hoff;
 // src may be reused on return.  Callers queuing several copies grow h_in for all of them first.
 void to_device(Ctx* c, uint8_t* d_dst, const void* src, size_t n, size_t hoff = 0) {
@@ -362,7 +407,11 @@ constexpr size_t kMetaBytes = 64;
 
 uint8_t* zc(Ctx* c) {
     if (!c->h_zc) {
-        check(hipHostMalloc(reinterpret_cast<void**>(&c->h_zc), kZcBytes, hipHostMallocMapped), "hipHostMalloc(zc)");
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->h_zc), kZcBytes, hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            c->h_zc = nullptr;
+            throw std::bad_alloc();
+        }
         check(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_zc), c->h_zc, 0), "hipHostGetDevicePointer");
     }
     return c->h_zc;
@@ -515,13 +564,7 @@ bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* a
 }
 }  // namespace
 
-// src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes.
-extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize) {
-    const size_t U = origSize;
-    if (U == 0 || too_big("RLEcompress", U)) {
-        *compressedSize = 0;
-        return U == 0 ? static_cast<char*>(calloc(16, 1)) : nullptr;
-    }
+static char* compress_impl(char* data, size_t U, size_t* compressedSize) {
     Ctx* c = ctx();
     if (U < kSegEncodeBytes) {   // one wave walks it: the single-copy path
         const uint64_t t0 = now_ns();
@@ -565,16 +608,25 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
     return r;
 }
 
-// src/rleCompression.c:47-62 — returns a malloc block of U+E bytes (decoded U, then E zeros).
-extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompressedSize, size_t extraAllocation) {
-    const size_t C = compressedSize, U = uncompressedSize, E = extraAllocation, total = U + E;
-    if (too_big("RLEdecompress", C) || too_big("RLEdecompress", U)) return nullptr;
-    char* r = static_cast<char*>(malloc(total ? total : 1));
-    if (!r) return nullptr;
-    if (C == 0) {  // nothing to decode: calloc'd block (:48)
-        memset(r, 0, total);
-        return r;
+// src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes; NULL (errno
+// = ENOMEM) when an allocation fails, as the reference's calloc can (:10).
+extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize) {
+    const size_t U = origSize;
+    if (U == 0 || too_big("RLEcompress", U)) {
+        *compressedSize = 0;
+        return U == 0 ? static_cast<char*>(calloc(16, 1)) : nullptr;
     }
+    try {
+        return compress_impl(data, U, compressedSize);
+    } catch (const std::bad_alloc&) {
+        drain_after_oom();
+        *compressedSize = 0;
+        return nullptr;
+    }
+}
+
+static void decompress_impl(char* data, size_t C, size_t U, size_t E, char* r) {
+    const size_t total = U + E;
     Ctx* c = ctx();
     if (C < kSegDecodeBytes && total <= kOneTripBytes) {   // one wave walks it: the single-copy path
         const uint64_t t0 = now_ns();
@@ -585,7 +637,7 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
         g_stats.bytes_h2d += round16(C) + kMetaBytes;
         g_stats.bytes_d2h += round16(total) + kMetaBytes;
         g_stats.ns_device += now_ns() - t0;
-        return r;
+        return;
     }
     grow_dev(c->d_in, c->d_in_cap, round16(C));
     grow_dev(c->d_out, c->d_out_cap, round16(total));
@@ -616,21 +668,33 @@ extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompr
     g_stats.ns_stage_in += t1 - t0;
     g_stats.ns_device += t2 - t1;
     g_stats.ns_stage_out += t3 - t2;
-    return r;
+}
+
+// src/rleCompression.c:47-62 — returns a malloc block of U+E bytes (decoded U, then E zeros); NULL
+// (errno = ENOMEM) when an allocation fails, as the reference's calloc can (:48).
+extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompressedSize, size_t extraAllocation) {
+    const size_t C = compressedSize, U = uncompressedSize, E = extraAllocation, total = U + E;
+    if (too_big("RLEdecompress", C) || too_big("RLEdecompress", U)) return nullptr;
+    char* r = static_cast<char*>(malloc(total ? total : 1));
+    if (!r) return nullptr;
+    if (C == 0) {  // nothing to decode: calloc'd block (:48)
+        memset(r, 0, total);
+        return r;
+    }
+    try {
+        decompress_impl(data, C, U, E, r);
+        return r;
+    } catch (const std::bad_alloc&) {
+        drain_after_oom();
+        free(r);
+        return nullptr;
+    }
 }
 
 // src/filesystemApi.c:766-775 (decode, append, re-encode) fused into one device
 // round trip whose re-encode covers only c^r ‖ newContent (include/rle_fileops.h).
-extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompressedSize, const char* newContent,
-                           size_t newContentLen, size_t* newCompressedSize) {
-    const size_t C = contentSize, U = uncompressedSize, A = newContentLen;
-    // U == 0: the decode keeps nothing below U and whatever it writes into the extra region is
-    // overwritten by the appended bytes (:767-770), so the result is encode(newContent)
-    if (U == 0) return RLEcompress(const_cast<char*>(newContent), A, newCompressedSize);
-    if (too_big("RLEappend", C) || too_big("RLEappend", U + A)) {
-        *newCompressedSize = 0;
-        return nullptr;
-    }
+static char* append_impl(char* content, size_t C, size_t U, const char* newContent, size_t A,
+                         size_t* newCompressedSize) {
     Ctx* c = ctx();
     if (C && C < kSegDecodeBytes && 16 + A < kSegEncodeBytes &&
         rle_max_compressed_size(16 + A) <= kOneTripBytes) {
@@ -658,7 +722,8 @@ extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompresse
     }
     const size_t offA = round16(C) + 16;   // d_in: old stream | splice head (16 B) | new bytes
     const size_t inBytes = offA + A;
-    grow_host(c->h_in, c->h_in_cap, inBytes);
+    // pinned staging only for the copies to_device stages (both, before either is queued)
+    grow_host(c->h_in, c->h_in_cap, std::max(staged(A) ? inBytes : 0, staged(C) ? C : 0));
     grow_dev(c->d_in, c->d_in_cap, round16(inBytes));
     grow_dev(c->d_mid, c->d_mid_cap, round16(U + A));
     const uint64_t t0 = now_ns();
@@ -715,55 +780,66 @@ extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompresse
     return out;
 }
 
-// SURVEY.md §8 (f2)/(f4): readNFilesHandler's decode loop (src/filesystemApi.c:675-687) and the
-// eviction loop (src/server.c:314-323) as one batched launch (include/rle_fileops.h).
-extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compressedSize,
-                              const size_t* uncompressedSize, char* const* out) {
-    if (n == 0) return 0;
-    if (!data || !compressedSize || !uncompressedSize || !out) {
-        errno = EINVAL;
-        return -1;
+extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompressedSize, const char* newContent,
+                           size_t newContentLen, size_t* newCompressedSize) {
+    const size_t C = contentSize, U = uncompressedSize, A = newContentLen;
+    // U == 0: the decode keeps nothing below U and whatever it writes into the extra region is
+    // overwritten by the appended bytes (:767-770), so the result is encode(newContent)
+    if (U == 0) return RLEcompress(const_cast<char*>(newContent), A, newCompressedSize);
+    if (too_big("RLEappend", C) || too_big("RLEappend", U + A)) {
+        *newCompressedSize = 0;
+        return nullptr;
     }
-    std::vector<size_t> idx;
-    size_t inTot = 0, outTot = 0, maxC = 0;
     try {
-        idx.reserve(n);
-    } catch (...) {
-        errno = ENOMEM;
-        return -1;
+        return append_impl(content, C, U, newContent, A, newCompressedSize);
+    } catch (const std::bad_alloc&) {
+        drain_after_oom();
+        *newCompressedSize = 0;
+        return nullptr;
     }
-    for (size_t i = 0; i < n; ++i) {
-        const size_t C = compressedSize[i], U = uncompressedSize[i];
-        if (C == 0) {  // calloc'd block (src/rleCompression.c:48)
-            if (U) memset(out[i], 0, U);
-            continue;
-        }
-        if (!data[i] || (U && !out[i])) {
-            errno = EINVAL;
-            return -1;
-        }
-        if (too_big("RLEdecompressN", C) || too_big("RLEdecompressN", U)) return -1;
-        idx.push_back(i);
-        inTot += round16(C);
-        outTot += round16(U);
-        maxC = C > maxC ? C : maxC;
-    }
-    const size_t m = idx.size();
-    if (m == 0) return 0;
-    if (m > (1u << 30)) {
-        errno = EINVAL;
-        return -1;
+}
+
+namespace {
+struct NTotals {
+    size_t cin = 0, uout = 0, h2d = 0, d2h = 0;
+    uint64_t ns_in = 0, ns_dev = 0, ns_out = 0;
+};
+
+// RLEdecompressN of one file too large for the bounded staging: straight from / to caller memory.
+void decompress_n_alone(Ctx* c, const char* data, size_t C, size_t U, char* out, NTotals& t) {
+    grow_dev(c->d_in, c->d_in_cap, round16(C));
+    grow_dev(c->d_out, c->d_out_cap, round16(U));
+    const uint64_t t0 = now_ns();
+    to_device(c, c->d_in, data, C);
+    const uint64_t t1 = now_ns();
+    queue_decode(c, c->d_in, C, c->d_out, U, U);
+    from_device(c, out, c->d_out, U);
+    if ((uint32_t)c->h_meta[kMetaDec + 5] & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompressN");
+    t.ns_in += t1 - t0;
+    t.ns_dev += now_ns() - t1;
+    t.h2d += C;
+    t.d2h += U;
+}
+
+// RLEdecompressN of the files idx[0, m) (each C > 0), staged together: one H2D, one launch per
+// kernel form, one D2H.  Their staged sizes sum to at most g_stage_cap each way.
+void decompress_n_chunk(Ctx* c, size_t* idx, size_t m, char* const* data, const size_t* compressedSize,
+                        const size_t* uncompressedSize, char* const* out, NTotals& t) {
+    size_t inTot = 0, outTot = 0, maxC = 0;
+    for (size_t k = 0; k < m; ++k) {
+        inTot += round16(compressedSize[idx[k]]);
+        outTot += round16(uncompressedSize[idx[k]]);
+        maxC = std::max(maxC, compressedSize[idx[k]]);
     }
     // files from kSegDecodeBytes up go to the segmented form, the rest to the one-wave kernel: the
     // large ones are packed first so that each launch takes a contiguous part of the metadata
     const size_t mL = maxC >= kSegDecodeBytes
-                          ? (size_t)(std::stable_partition(idx.begin(), idx.end(),
+                          ? (size_t)(std::stable_partition(idx, idx + m,
                                                            [&](size_t i) { return compressedSize[i] >= kSegDecodeBytes; }) -
-                                     idx.begin())
+                                     idx)
                           : 0;
     size_t inLarge = 0;
     for (size_t k = 0; k < mL; ++k) inLarge += round16(compressedSize[idx[k]]);
-    Ctx* c = ctx();
     // per-file metadata, one pinned block: in_off, in_len, out_off, out_len (m u64 each), status (m u32)
     const size_t metaBytes = 32 * m + 4 * m;
     grow_host(c->h_bm, c->h_bm_cap, metaBytes);
@@ -772,6 +848,7 @@ extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compres
     grow_host(c->h_out, c->h_out_cap, outTot);
     grow_dev(c->d_in, c->d_in_cap, inTot);
     grow_dev(c->d_out, c->d_out_cap, outTot);
+    if (mL) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes((uint32_t)mL, inLarge));
     const uint64_t t0 = now_ns();
     uint64_t* hb = reinterpret_cast<uint64_t*>(c->h_bm);
     size_t io = 0, oo = 0;
@@ -787,12 +864,9 @@ extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compres
     uint32_t* d_status = reinterpret_cast<uint32_t*>(db + 4 * m);
     check(hipMemcpyAsync(c->d_in, c->h_in, inTot, hipMemcpyHostToDevice, c->s), "H2D");
     check(hipMemcpyAsync(db, hb, 32 * m, hipMemcpyHostToDevice, c->s), "H2D(meta)");
-    if (mL) {
-        grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes((uint32_t)mL, inLarge));
-        if (rle_decode_batch_device_seg(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr, d_status,
-                                        (uint32_t)mL, inLarge, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
-            die("decode launch", hipGetLastError());
-    }
+    if (mL && rle_decode_batch_device_seg(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr, d_status,
+                                          (uint32_t)mL, inLarge, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
+        die("decode launch", hipGetLastError());
     if (m > mL && rle_decode_batch_device(c->d_in, db + mL, db + m + mL, c->d_out, db + 2 * m + mL, db + 3 * m + mL,
                                           nullptr, d_status + mL, (uint32_t)(m - mL), c->s) != RLE_OK)
         die("decode launch", hipGetLastError());
@@ -801,24 +875,92 @@ extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compres
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     const uint64_t t2 = now_ns();
     const uint32_t* hst = reinterpret_cast<const uint32_t*>(hb + 4 * m);
-    size_t cin = 0, uout = 0;
     for (size_t k = 0; k < m; ++k) {
         const size_t i = idx[k], U = uncompressedSize[i];
         if (U) memcpy(out[i], c->h_out + hb[2 * m + k], U);
         if (hst[k] & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompressN");
-        cin += compressedSize[i];
-        uout += U;
     }
-    const uint64_t t3 = now_ns();
-    g_stats.calls_decompress += m;
-    g_stats.bytes_in += cin;
-    g_stats.bytes_out += uout;
-    g_stats.bytes_h2d += inTot;
-    g_stats.bytes_d2h += outTot;
-    g_stats.ns_stage_in += t1 - t0;
-    g_stats.ns_device += t2 - t1;
-    g_stats.ns_stage_out += t3 - t2;
+    t.ns_in += t1 - t0;
+    t.ns_dev += t2 - t1;
+    t.ns_out += now_ns() - t2;
+    t.h2d += inTot;
+    t.d2h += outTot;
+}
+
+int decompress_n_impl(size_t n, char* const* data, const size_t* compressedSize, const size_t* uncompressedSize,
+                      char* const* out) {
+    std::vector<size_t> idx;
+    idx.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+        const size_t C = compressedSize[i], U = uncompressedSize[i];
+        if (C == 0) {  // calloc'd block (src/rleCompression.c:48)
+            if (U) memset(out[i], 0, U);
+            continue;
+        }
+        if (!data[i] || (U && !out[i])) {
+            errno = EINVAL;
+            return -1;
+        }
+        if (too_big("RLEdecompressN", C) || too_big("RLEdecompressN", U)) return -1;
+        idx.push_back(i);
+    }
+    if (idx.empty()) return 0;
+    Ctx* c = ctx();
+    NTotals t;
+    // files in batch order: chunks of consecutive files that fit the staging together, files too
+    // large for it alone
+    size_t k0 = 0, inTot = 0, outTot = 0;
+    for (size_t k = 0; k <= idx.size(); ++k) {
+        const bool end = k == idx.size();
+        const size_t Ci = end ? 0 : round16(compressedSize[idx[k]]), Ui = end ? 0 : round16(uncompressedSize[idx[k]]);
+        const bool alone = !end && (Ci > g_stage_cap || Ui > g_stage_cap);
+        if (end || alone || inTot + Ci > g_stage_cap || outTot + Ui > g_stage_cap) {
+            if (k > k0) decompress_n_chunk(c, idx.data() + k0, k - k0, data, compressedSize, uncompressedSize, out, t);
+            k0 = k;
+            inTot = outTot = 0;
+        }
+        if (alone) {
+            const size_t i = idx[k];
+            decompress_n_alone(c, data[i], compressedSize[i], uncompressedSize[i], out[i], t);
+            k0 = k + 1;
+            continue;
+        }
+        inTot += Ci;
+        outTot += Ui;
+    }
+    for (size_t i : idx) {
+        t.cin += compressedSize[i];
+        t.uout += uncompressedSize[i];
+    }
+    g_stats.calls_decompress += idx.size();
+    g_stats.bytes_in += t.cin;
+    g_stats.bytes_out += t.uout;
+    g_stats.bytes_h2d += t.h2d;
+    g_stats.bytes_d2h += t.d2h;
+    g_stats.ns_stage_in += t.ns_in;
+    g_stats.ns_device += t.ns_dev;
+    g_stats.ns_stage_out += t.ns_out;
     return 0;
+}
+}  // namespace
+
+// SURVEY.md §8 (f2)/(f4): readNFilesHandler's decode loop (src/filesystemApi.c:675-687) and the
+// eviction loop (src/server.c:314-323) as batched launches (include/rle_fileops.h).  Files are
+// staged in bounded chunks (g_stage_cap), so the pinned memory a worker thread holds does not grow
+// with the batch.
+extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compressedSize,
+                              const size_t* uncompressedSize, char* const* out) {
+    if (n == 0) return 0;
+    if (!data || !compressedSize || !uncompressedSize || !out) {
+        errno = EINVAL;
+        return -1;
+    }
+    try {
+        return decompress_n_impl(n, data, compressedSize, uncompressedSize, out);
+    } catch (const std::bad_alloc&) {
+        drain_after_oom();
+        return -1;
+    }
 }
 
 extern "C" int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset) {

@@ -102,6 +102,49 @@ def test_decompress_n_reference_semantics_on_odd_streams():
         assert g == O.decode(s, u)[0], (s, u)
         assert g == R.decompress(s, u), (s, u)
     assert R.decompress_n([], []) == []
+    # U == 0 with a non-empty stream: nothing is decoded (the reference writes into a calloc(0)
+    # block); one-wave and segmented stream sizes, with and without an extra region
+    big = O.encode(O.gen(1, 3, 40000))
+    for s in (b"aa9", b"abc", big):
+        assert R.decompress_n([s], [0]) == [b""]
+        assert R.decompress(s, 0) == b""
+        # with an extra region the reference's unbounded first write (src/rleCompression.c:51)
+        # lands in it: the oracle restates that
+        assert R.decompress(s, 0, 5) == O.decode(s, 0, 5)[0][:5]
+    assert R.decompress_n([b"aa9", big, b"", b"ab"], [0, 0, 0, 1]) == [b"", b"", b"", b"a"]
+
+
+def test_decompress_n_chunks_past_the_staging_cap():
+    # a readN larger than the bounded staging (kStageCap, 32 MiB): consecutive chunks, and a file
+    # too large for the staging decoded straight into the caller's buffer
+    xs = [O.gen(1 + i % 4, 500 + i, (1 << 20) + 37 * i) for i in range(40)]
+    xs.insert(17, bytes(48 << 20))
+    xs.append(b"q" * 5)
+    ys = [O.encode(x) if i % 7 else R.compress(x) for i, x in enumerate(xs)]
+    got = R.decompress_n(ys, [len(x) for x in xs])
+    bad = [i for i in range(len(xs)) if got[i] != xs[i]]
+    assert not bad, bad[:5]
+
+
+def test_decompress_n_small_staging_cap_subprocess():
+    # the same chunking with a 64 KiB cap (RLE_MI355X_STAGE_CAP), in a fresh process so the cap
+    # is read at library init: many small chunks, and mid-size files alone
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = sys.argv[1:3]\n"
+        "import rle_mi355x as R, rle_oracle as O\n"
+        "xs = [O.gen(i % 5, 900 + i, (i * 7919) % 90000) for i in range(120)]\n"
+        "got = R.decompress_n([O.encode(x) for x in xs], [len(x) for x in xs])\n"
+        "assert got == xs, [i for i in range(len(xs)) if got[i] != xs[i]][:5]\n"
+        "print('ok')\n")
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, RLE_MI355X_STAGE_CAP=str(64 << 10))
+    r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "c-filestorage-server-and-client_amd"),
+                        os.path.join(root, "oracle")], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
 
 
 def test_decompress_n_readn_batch_of_fixture_files(dummyfiles):
