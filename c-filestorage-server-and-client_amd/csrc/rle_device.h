@@ -675,6 +675,50 @@ __device__ __forceinline__ u32 sswz(u32 t) {
 }
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
+// One 32-byte staging chunk (16 u16 keys) at s4, through the staging swizzle.
+__device__ __forceinline__ void dec_read_chunk(const u32x4* s4, u32x4& a, u32x4& b) {
+    if (RLE_SWZ == 1) {
+        const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
+        auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
+        a = u32x4{rd(0), rd(1), rd(2), rd(3)};
+        b = u32x4{rd(4), rd(5), rd(6), rd(7)};
+    } else if (RLE_SWZ == 2) {
+        a = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4)));
+        b = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4) + 16u));
+    } else {
+        a = s4[0];
+        b = s4[1];
+    }
+}
+
+// The flush's fill of one 32-byte staging chunk (16 u16 keys a, b): the position index p goes into
+// bits 8..11 of each key (empty slots get the index alone, below every key and below the carry),
+// and a packed-u16 prefix max inside the chunk carries each flagged key over the run it starts.
+__device__ __forceinline__ void dec_fill_scan(u32x4 a, u32x4 b, u32 (&L)[8]) {
+    L[0] = a.x | 0x01000000u; L[1] = a.y | 0x03000200u; L[2] = a.z | 0x05000400u; L[3] = a.w | 0x07000600u;
+    L[4] = b.x | 0x09000800u; L[5] = b.y | 0x0B000A00u; L[6] = b.z | 0x0D000C00u; L[7] = b.w | 0x0F000E00u;
+    if (!(RLE_ABL & 4)) {
+        // running max of the even positions (low halves) and of the odd ones (high halves) ...
+#pragma unroll
+        for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], L[m - 1]);
+        // ... then position 2m takes the odd max up to 2m-1, position 2m+1 the even max up to 2m
+#pragma unroll
+        for (u32 m = 7; m > 0; --m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m], L[m - 1], 0x05040302u));
+        L[0] = pkmax(L[0], L[0] << 16);
+    }
+}
+// The chunk's 16 output bytes: each position's latest key at or before it, else the byte `carry`
+// entering the chunk (a run entering a chunk covers at most its first 8 positions, dwords 0..3).
+__device__ __forceinline__ u32x4 dec_fill_out(const u32 (&L)[8], u32 carry) {
+    const u32 crep = carry | 0x10001000u | (carry << 16);
+    u32x4 o;
+    o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
+    o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
+    o.z = __builtin_amdgcn_perm(L[5], L[4], 0x06040200u);
+    o.w = __builtin_amdgcn_perm(L[7], L[6], 0x06040200u);
+    return o;
+}
+
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
                                          u32& head, uint8_t* dst, Stamps& sp) {
@@ -691,42 +735,12 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
         // (a lane's carry comes from the lane before it, and the active lanes are 0..nfl-1), so no
         // stored byte depends on it.
         u32x4 a, b;
-        if (RLE_SWZ == 1) {
-            const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
-            auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
-            a = u32x4{rd(0), rd(1), rd(2), rd(3)};
-            b = u32x4{rd(4), rd(5), rd(6), rd(7)};
-        } else if (RLE_SWZ == 2) {
-            a = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4)));
-            b = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4) + 16u));
-        } else {
-            a = s4[0];
-            b = s4[1];
-        }
+        dec_read_chunk(s4, a, b);
         RLE_STAMP(sp, 3);   // flush: staging reads
-        // position index p (bits 8..11 of each u16) into each key; empty slots get the index alone,
-        // below every key and below the carry
-        u32 L[8] = {a.x | 0x01000000u, a.y | 0x03000200u, a.z | 0x05000400u, a.w | 0x07000600u,
-                    b.x | 0x09000800u, b.y | 0x0B000A00u, b.z | 0x0D000C00u, b.w | 0x0F000E00u};
-        // prefix max of the keys inside the chunk: within each pair, then across pairs
-        if (!(RLE_ABL & 4)) {
-            // running max of the even positions (low halves) and of the odd ones (high halves) ...
-#pragma unroll
-            for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], L[m - 1]);
-            // ... then position 2m takes the odd max up to 2m-1, position 2m+1 the even max up to 2m
-#pragma unroll
-            for (u32 m = 7; m > 0; --m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m], L[m - 1], 0x05040302u));
-            L[0] = pkmax(L[0], L[0] << 16);
-        }
+        u32 L[8];
+        dec_fill_scan(a, b, L);
         const u32 lastb = (L[7] >> 16) & 0xFFu;   // byte of the chunk's last key = its last output byte
-        const u32 carry = from_prev_lane(lastb, fillc);
-        // a run entering the chunk covers at most its first 8 positions (dwords 0..3)
-        const u32 crep = carry | 0x10001000u | (carry << 16);
-        u32x4 o;
-        o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
-        o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
-        o.z = __builtin_amdgcn_perm(L[5], L[4], 0x06040200u);
-        o.w = __builtin_amdgcn_perm(L[7], L[6], 0x06040200u);
+        const u32x4 o = dec_fill_out(L, from_prev_lane(lastb, fillc));
         RLE_STAMP(sp, 4);   // flush: fill + carry
         const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
         vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o, wt);   // RLE_NOSTORE: diagnostic
@@ -999,22 +1013,28 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
     const u32 rel = st.out_pos - st.flushed;   // < 16
     const u32 span = end - st.flushed;
     const u32 nq = (span + 15u) >> 4;
-    const u32 tv = st.tail & 0xFFu;
-    const u32 c1 = lds_addr(stage) + 32u;   // staging chunk 1
+    const u32 tv = rep4(st.tail & 0xFFu);
+    // chunk 0: the staged positions [0, rel) filled like a flush (every lane computes it from the
+    // same two broadcast reads), the rest the tail byte
+    u32x4 a, b;
+    dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), a, b);
+    u32 L[8];
+    dec_fill_scan(a, b, L);
+    const u32x4 f = dec_fill_out(L, st.fillc);
+    const u32 fv[4] = {f.x, f.y, f.z, f.w};
+    u32 c0[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 nb = rel > 4u * k ? (rel - 4u * k < 4u ? rel - 4u * k : 4u) : 0u;
+        const u32 m = lowmask(8u * nb);
+        c0[k] = (fv[k] & m) | (tv & ~m);
+    }
     for (u32 q0 = 0; q0 < nq; q0 += kWave) {
         const u32 q = q0 + lane;
         if (q < nq) {
-            u32 ob[4] = {0u, 0u, 0u, 0u};
-            u32 cur = st.fillc;
-            for (u32 j = 0; j < 16u; ++j) {
-                u32 v = tv;
-                if (q == 0u && j < rel) {
-                    const u32 h = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(sswz(c1 + 2u * j));
-                    cur = (h & kKeyFlag) ? (h & 0xFFu) : cur;
-                    v = cur;
-                }
-                ob[j >> 2] |= v << (8u * (j & 3u));
-            }
+            u32 ob[4];
+#pragma unroll
+            for (u32 k = 0; k < 4; ++k) ob[k] = q == 0u ? c0[k] : tv;
             const u32 j0 = q == 0u ? st.head : 0u;
             if (16u * q + 16u <= span && j0 == 0u) {
                 u32x4 o;

@@ -28,6 +28,49 @@ __device__ __forceinline__ u32 xcd_buffer(u32 wg, u32 ngrid, u32 waves, u32 wid)
 #define RLE_NOWALK 0
 #endif
 
+#ifndef RLE_STAGGER   // experiments: the waves sharing a SIMD start RLE_STAGGER * 64 cycles apart
+#define RLE_STAGGER 0
+#endif
+__device__ __forceinline__ void stagger() {
+#if RLE_STAGGER
+    const u32 slot = (u32)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) & 3u;   // HW_ID.WAVE_ID
+    for (u32 k = 0; k < slot; ++k) __builtin_amdgcn_s_sleep(RLE_STAGGER);
+#endif
+}
+
+// Diagnostic timeline builds (RLE_TIMELINE=1, never the product library): lane 0 of the wave of
+// buffer b < kTlWaves records s_memrealtime (100 MHz) at kernel entry [0], walk start [1], the start
+// of each of its first 8 tiles [2..9] and the end [10], plus HW_ID [11] and XCC_ID [12];
+// rle_mi355x_timeline() reads them.
+#ifndef RLE_TIMELINE
+#define RLE_TIMELINE 0
+#endif
+#if RLE_TIMELINE
+constexpr u32 kTlWaves = 16384, kTlEv = 16;
+static __device__ unsigned long long g_tl[kTlWaves * kTlEv];
+__device__ __forceinline__ void tl_mark(u32 b, u32 ev, u32 lane) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0u && b < kTlWaves && ev < kTlEv) g_tl[b * kTlEv + ev] = t;
+}
+__device__ __forceinline__ unsigned long long tl_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void tl_put(u32 b, u32 ev, unsigned long long t, u32 lane) {
+    if (lane == 0u && b < kTlWaves) g_tl[b * kTlEv + ev] = t;
+}
+__device__ __forceinline__ void tl_ids(u32 b, u32 lane) {
+    const u32 hw = (u32)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_ID
+    const u32 xcc = (u32)__builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // XCC_ID
+    if (lane == 0u && b < kTlWaves) {
+        g_tl[b * kTlEv + 11] = hw;
+        g_tl[b * kTlEv + 12] = xcc;
+    }
+}
+#else
+__device__ __forceinline__ unsigned long long tl_now() { return 0; }
+__device__ __forceinline__ void tl_put(u32, u32, unsigned long long, u32) {}
+__device__ __forceinline__ void tl_mark(u32, u32, u32) {}
+__device__ __forceinline__ void tl_ids(u32, u32) {}
+#endif
+
 #ifndef RLE_ENC_WAVES
 #define RLE_ENC_WAVES 4
 #endif
@@ -44,6 +87,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ out_off,
                                                            uint64_t* __restrict__ out_len,
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+    const unsigned long long tl0 = tl_now();
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * 2 * kEncSlot];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kEncWaves * kEncStage];
     const u32 lane = threadIdx.x & (kWave - 1);
@@ -52,6 +96,9 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     const uint8_t* slots = slots_all + wid * 2 * kEncSlot;
     const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kEncWaves, wid);
     if (b >= n) return;
+    tl_mark(b, 0, lane);
+    tl_put(b, 13, tl0, lane);
+    tl_ids(b, lane);
     const uint64_t U64 = in_len[b];
     const uint8_t* src = in + in_off[b];
     uint8_t* dst = out + out_off[b];
@@ -73,14 +120,18 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
     st.sp.last = memtime();
 #endif
+    stagger();
+    tl_mark(b, 1, lane);
     // 1024-byte tiles where they save a tile, up to kEncSmall (rle_device.h, enc_tile<true>)
     if (enc_ntiles_for(U) < ntiles_for(U) && U <= kEncSmall)
         walk_tiles<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
                                    [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                                       tl_mark(b, 2u + t, lane);
                                        return enc_tile<true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc);
                                    });
     else
         walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+            tl_mark(b, 2u + t, lane);
             return enc_tile<false>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc);
         });
     RLE_STAMP(st.sp, 6);   // drain
@@ -90,6 +141,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
         out_len[b] = st.out_pos;
         if (status) status[b] = RLE_STATUS_OK;
     }
+    tl_mark(b, 10, lane);
     RLE_STAMP(st.sp, 7);   // finish
 #if RLE_STAMPS
     if (lane == 0) {
@@ -215,6 +267,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ out_cap,
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt,
                                                            const uint32_t* __restrict__ order) {
+    const unsigned long long tl0 = tl_now();
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kDecStage];
     __shared__ DecEntry tbl[256];
@@ -243,6 +296,9 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     }
     // all five per-buffer words are loaded at once, unconditionally (index clamped; n >= 1)
     const u32 bi = b < n ? b : 0u;
+    tl_mark(b, 0, lane);
+    tl_put(b, 13, tl0, lane);
+    tl_ids(b, lane);
     const uint64_t* capp = out_cap ? out_cap : out_len;
     const uint64_t C64 = in_len[bi], U64 = out_len[bi], cap = capp[bi];
     const uint8_t* src = in + in_off[bi];
@@ -256,6 +312,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
 #pragma unroll
     for (u32 i = 0; i < kTblPer; ++i) tbl[(threadIdx.x + i * kDecBlock) & 255u] = te[i];
+    stagger();
     walk_prime(rsi, 0u, ntiles, lane, slots);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
@@ -274,9 +331,11 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
         st.sp.last = memtime();
 #endif
+        tl_mark(b, 1, lane);
         const bool serial = walk_tiles(
             rsi, 0u, ntiles, lane, slots,
             [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                tl_mark(b, 2u + t, lane);
                 return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc);
             },
             true);
@@ -295,6 +354,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         }
 #endif
         if (lane == 0 && status) status[b] = stat;
+        tl_mark(b, 10, lane);
     }
 }
 
@@ -481,6 +541,21 @@ extern "C" int rle_mi355x_selftest(void) {
     (void)hipFree(d);
     if (e1 != hipSuccess) return RLE_E_HIP;
     return (int)h;
+}
+
+extern "C" int rle_mi355x_timeline(unsigned long long* out, int reset) {
+#if RLE_TIMELINE
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(rle::g_tl), sizeof(rle::g_tl)) != hipSuccess) return RLE_E_HIP;
+    if (reset) {
+        static unsigned long long z[rle::kTlWaves * rle::kTlEv];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rle::g_tl), z, sizeof(z)) != hipSuccess) return RLE_E_HIP;
+    }
+    return RLE_OK;
+#else
+    (void)out;
+    (void)reset;
+    return RLE_E_INVAL;   // not a diagnostic build
+#endif
 }
 
 extern "C" int rle_mi355x_stamps(unsigned long long* out, int reset) {

@@ -125,6 +125,11 @@ int rle_append_prepare_device(const void* d_mid, uint64_t U, void* d_head, uint6
  * move/drain/finish, waves]; RLE_E_INVAL otherwise. */
 int rle_mi355x_stamps(unsigned long long* out9, int reset);
 
+/* Diagnostic builds only (RLE_TIMELINE=1, never the product library): per-buffer wave timelines of
+ * the one-wave batch kernels, 16384 x 16 u64 (s_memrealtime at entry, walk start, tiles 0..7, end;
+ * HW_ID, XCC_ID); RLE_E_INVAL otherwise. */
+int rle_mi355x_timeline(unsigned long long* out, int reset);
+
 /* Number of visible HIP devices (0 when none). */
 int rle_mi355x_device_count(void);
 
