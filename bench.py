@@ -96,6 +96,10 @@ class Batch:
         i64 = lambda v: torch.tensor(v, dtype=torch.int64, device=dev)
         self.n = n
         self.sizes = sizes
+        # the batch's largest buffer (the sized entry points pick the cooperative small-buffer
+        # kernels from it); the largest compressed size is known once the batch has been encoded
+        self.max_u = max(sizes)
+        self.max_c = R.max_compressed_size(self.max_u)
         self.u_bytes = sum(sizes)
         self.offs, self.lens = i64(offs), i64(sizes)
         self.coffs = i64(coffs)
@@ -118,7 +122,7 @@ class Batch:
                                total_in_bytes=self.u_bytes, workspace=self.ws_enc, stream=stream)
         else:
             R.encode_batch(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status,
-                           stream=stream)
+                           stream=stream, max_len=self.max_u)
 
     def decode(self, stream=None):
         if self.seg:
@@ -126,7 +130,12 @@ class Batch:
                                total_in_bytes=self.c_cap, workspace=self.ws_dec, stream=stream)
         else:
             R.decode_batch(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
-                           stream=stream)
+                           stream=stream, max_in_len=self.max_c, max_out_len=self.max_u)
+
+    def calibrate(self):
+        """After an encode: the largest compressed size, as a file server knows from its stored sizes."""
+        torch.cuda.synchronize()
+        self.max_c = int(self.clen.max().item())
 
 
 def time_kernels(fn, reps, stream):
@@ -226,6 +235,8 @@ def main():
                 gathered[k].record(comm)
         B.decode(stream)
 
+    B.encode(stream)
+    B.calibrate()
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
@@ -279,7 +290,7 @@ def main():
         torch.cuda.empty_cache()
         N = Batch(WORKLOADS["dec64k"], 0, 1, dev)
         N.encode(stream)
-        torch.cuda.synchronize()
+        N.calibrate()
         nc = int(N.clen.sum().item())
         td = time_kernels(lambda: N.decode(stream), 20, stream)
         te = time_kernels(lambda: N.encode(stream), 20, stream)

@@ -1,0 +1,399 @@
+// rle_coop.hip — cooperative batch kernels for small buffers: one workgroup per buffer, one wave
+// per tile, the cross-tile state exchanged through LDS.
+//
+// The one-wave-per-buffer kernels (rle_kernels.hip) walk a buffer's tiles in sequence, so a batch
+// of few small buffers (configs[1]: 4096 x 4 KiB, 4-5 tiles each) gives each SIMD only 4 waves
+// whose tile steps are long dependent chains, and the SIMDs sit idle much of the time (DESIGN.md
+// §4, "Cooperative small-buffer kernels").  Here every tile of a buffer is its own wave, and the
+// sequential state of the reference's scan (src/rleCompression.c:9-62) crosses tiles in two
+// barrier-separated exchanges:
+//   decode  1. each wave: its tile's token-phase map                -> LDS; barrier
+//           2. entry phase = composition of the earlier tiles' maps; decoded length -> LDS; barrier
+//           3. scatter into one staging for the whole buffer at the prefix offset; barrier
+//           4. all waves fill and store the buffer's 16-byte output chunks
+//   encode  1. each wave: the last run boundary of its tile          -> LDS; barrier
+//           2. entry run start = max over the earlier tiles; token masks; compressed size -> LDS;
+//              barrier
+//           3. passes 1 and 2 into one staging at the prefix offset; barrier; all waves store it.
+// The tile steps are the one-wave kernels' (rle_device.h: enc_analyze_bounds / enc_tokens /
+// enc_pass1, dec_prepare / dec_lengths / dec_scatter / dec_fill_*), so the output is the same
+// bytes.  A buffer with more tiles than the workgroup has waves (or, decode, more decoded bytes
+// than its staging) is walked by wave 0 alone with the one-wave tile loop; streams the tiled path
+// declines take the exact serial decoder, as there.
+#include "rle_device.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+namespace rle {
+
+constexpr u32 kCoopMaxWaves = 8;
+
+__device__ __forceinline__ u32 coop_wave() { return uniform(threadIdx.x / kWave); }
+
+// ================================================================ ENCODE
+// kW waves; 1024-byte tiles (enc_tile<true> form), so buffers of up to 1024 kW bytes are coop.
+template <u32 kW>
+__global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len,
+                                                             uint8_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ out_off,
+                                                             uint64_t* __restrict__ out_len,
+                                                             uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+    constexpr u32 kUmax = kEncStep * kW;
+    // output position r at byte 16 + r (chunk 0: guard of the non-starts' back-writes); +32: the
+    // writes of positions past U land at the output end
+    constexpr u32 kStageC = 16u + kUmax + kUmax / 2u + 32u;
+    constexpr u32 kStage = ((kStageC > kEncStage ? kStageC : kEncStage) + 127u) & ~127u;
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kW * kEncSlot];
+    __shared__ __attribute__((aligned(128))) uint8_t stage[kStage];
+    __shared__ u32 xch[2 * kW];   // [0, kW) last run boundary per tile, [kW, 2kW) compressed size
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = coop_wave();
+    const u32 b = blockIdx.x;
+    if (b >= n) return;
+    const uint64_t U64 = in_len[b];
+    const uint8_t* src = in + in_off[b];
+    uint8_t* dst = out + out_off[b];
+    u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+    if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+    if (bad) {
+        if (threadIdx.x == 0) {
+            out_len[b] = 0;
+            if (status) status[b] = bad;
+        }
+        return;
+    }
+    const u32 U = (u32)U64;
+    const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U + U / 2u);
+    const EncK kc = enc_k();
+    const u32 ntiles = enc_ntiles_for(U);
+    if (ntiles > kW) {   // too long for one round: wave 0 walks it like encode_kernel
+        if (wid != 0u) return;
+        EncState st{0u, 0u, 0u, 0u, 0u, wt != 0u, {}};
+        if (U <= 16384u)   // rle_kernels.hip kEncSmall
+            walk_tiles<kEncStep, true>(rsi, 0u, enc_ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                return enc_tile<true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc);
+            });
+        else
+            walk_tiles(rsi, 0u, ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                return enc_tile<false>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc);
+            });
+        if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
+        if (lane == 0) {
+            out_len[b] = st.out_pos;
+            if (status) status[b] = RLE_STATUS_OK;
+        }
+        return;
+    }
+    const u32 nact = ntiles ? ntiles : 1u;   // waves with a tile (wave 0 also for U = 0)
+    if (wid >= nact) return;                 // ended waves do not hold up s_barrier
+    const uint8_t* slot = slots + wid * kEncSlot;
+    const bool act = wid < ntiles;
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
+    if (act) Refill{rsi, kEncStep * wid + 16u * lane, uniform(lds_addr(slot)), true, lane == 0u}();
+    vm_drain();
+    __syncthreads();   // every tile has landed
+    EncAn an{};
+    if (act) {
+        const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
+        const uint2 look = *reinterpret_cast<const uint2*>(slot + kSlot);
+        // the input byte before the tile: the previous tile's last byte
+        const u32 prev_top = wid ? *reinterpret_cast<const u32*>(slot - kEncSlot + kSlot - 4u) & 0xFF000000u : 0u;
+        an = enc_analyze_bounds<true>(cur, look, kEncStep * wid, U, U, lane, prev_top, kc);
+        const u32 ilast = readlane(an.incl, kWave - 1u);   // last run boundary in the tile (0: none)
+        if (lane == 0) xch[wid] = ilast;
+    }
+    __syncthreads();
+    u32 nout = 0u, oincl = 0u;
+    if (act) {
+        u32 rs = 0u;   // start of the run holding the byte before the tile
+        for (u32 s = 0; s < wid; ++s) rs = xch[s] > rs ? xch[s] : rs;
+        enc_tokens(an, rs);
+        nout = bcnt(an.P, bcnt(an.P, bcnt(an.T, 0u)));
+        oincl = wave_scan_incl(nout, 0u, OpAdd());
+        if (lane == 0) xch[kW + wid] = readlane(oincl, kWave - 1u);
+    }
+    __syncthreads();
+    u32 O = 0u, total = 0u;
+    for (u32 s = 0; s < ntiles; ++s) {
+        const u32 c = xch[kW + s];
+        O += s < wid ? c : 0u;
+        total += c;
+    }
+    if (act) {
+        const u32* w = an.w;
+        const u32 T = an.T, P = an.P, B24 = an.B24, validm = an.validm;
+        const u32 NS = validm & ~T;
+        const u32 e0 = lds_addr(stage) + 16u + O + oincl - nout;
+        if (kEncStep * wid + kEncStep <= U) enc_pass1<true>(w, T, P, NS, e0, kc.V01);
+        else enc_pass1<false>(w, T, P, NS, e0, 0u);
+        // pass 2 (enc_tile): count digits, and second bytes whose position is the buffer's end
+        const u32 obase = 16u + O + oincl - nout;
+        u32 prem = P;
+        while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
+            if (prem) {
+                const u32 j = (u32)__builtin_ctz(prem);
+                prem &= prem - 1u;
+                const u32 mj = lowmask(j);
+                const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+                stage[oj + 2u] = (uint8_t)('1' + (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u));
+            }
+        }
+        const u32 vnext = (validm >> 1) | ((from_next_lane(validm, 0u) & 1u) << 15);
+        const u32 PX = P & ~vnext;
+        if (__builtin_amdgcn_ballot_w64(PX != 0u)) {
+            if (PX) {
+                const u32 j = (u32)__builtin_ctz(PX);
+                const u32 mj = lowmask(j);
+                const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+                const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
+                stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
+            }
+        }
+    }
+    __syncthreads();
+    // store: whole 16-byte chunks, then the final partial chunk byte by byte (nothing past C)
+    const u32 nthr = kWave * nact, t = threadIdx.x, nfull = total >> 4;
+    for (u32 c = t; c < nfull; c += nthr)
+        vstore(rso, 16u * c, *reinterpret_cast<const u32x4*>(stage + 16u + 16u * c), wt != 0u);
+    if (t < (total & 15u)) dst[16u * nfull + t] = stage[16u + 16u * nfull + t];
+    if (t == 0) {
+        out_len[b] = total;
+        if (status) status[b] = RLE_STATUS_OK;
+    }
+}
+
+// ================================================================ DECODE
+// kW waves (tiles of 1008 bytes: dec_tile's geometry); buffers decoding to at most kUmax bytes.
+template <u32 kW, u32 kUmax>
+__global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len,
+                                                             uint8_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ out_off,
+                                                             const uint64_t* __restrict__ out_len,
+                                                             const uint64_t* __restrict__ out_cap,
+                                                             uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+    // decoded position r at u16 16 + r (dec_tile's staging, one for the whole buffer); the one-wave
+    // fallback needs kDecStage
+    constexpr u32 kStageC = 2u * (16u + kUmax + 32u);
+    constexpr u32 kStage = ((kStageC > kDecStage ? kStageC : kDecStage) + 127u) & ~127u;
+    constexpr u32 kChunks = (kUmax + 15u) / 16u;
+    __shared__ __attribute__((aligned(16))) uint8_t slots[(kW > 2u ? kW : 2u) * kSlot];
+    __shared__ __attribute__((aligned(128))) uint8_t stage[kStage];
+    __shared__ DecEntry tbl[256];
+    __shared__ u32 xch[4 * kW];   // per tile: phase map, decoded length, serial, tail byte
+    __shared__ u32 lastb[kChunks + 1];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = coop_wave();
+    const u32 b = blockIdx.x;
+    if (b >= n) return;
+    for (u32 i = threadIdx.x; i < 256u; i += kWave * kW) tbl[i] = dec_entry_from(kDecTable.e[i]);
+    const uint64_t* capp = out_cap ? out_cap : out_len;
+    const uint64_t C64 = in_len[b], U64 = out_len[b], cap = capp[b];
+    const uint8_t* src = in + in_off[b];
+    uint8_t* dst = out + out_off[b];
+    u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
+    if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+    if (bad) {
+        if (threadIdx.x == 0 && status) status[b] = bad;
+        return;
+    }
+    const u32 C = (u32)C64, U = (u32)U64;
+    const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U);
+    const u32 ntiles = ntiles_for(C);
+    const DecK kc = dec_k();
+    __syncthreads();   // the phase table is complete
+    if (ntiles > kW || U > kUmax) {   // wave 0 walks it like decode_kernel
+        if (wid != 0u) return;
+        walk_prime(rsi, 0u, ntiles, lane, slots);
+        for (u32 k = lane; k < kDecStage / 16u; k += kWave) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
+        wave_lds_sync();
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, wt != 0u, {}};
+        const bool serial = walk_tiles(
+            rsi, 0u, ntiles, lane, slots,
+            [&](u32 t, const uint8_t* cs, const Refill& nx) { return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc); },
+            true);
+        u32 stat;
+        if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
+        else {
+            dec_finish(st, U, lane, stage, rso, dst);
+            stat = dec_tiled_status(st, U);
+        }
+        if (lane == 0 && status) status[b] = stat;
+        return;
+    }
+    const u32 nact = ntiles ? ntiles : 1u;
+    if (wid >= nact) return;   // ended waves do not hold up s_barrier
+    const uint8_t* slot = slots + wid * kSlot;
+    const bool act = wid < ntiles;
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
+    if (act) dma_tile(rsi, kTileStep * wid + 16u * lane, uniform(lds_addr(slot)));
+    // the staging positions this buffer can reach: [0, 16 + U + 17) u16
+    const u32 nz = (2u * (16u + U + 17u) + 15u) / 16u;
+    for (u32 k = threadIdx.x; k < nz; k += kWave * nact) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
+    vm_drain();
+    __syncthreads();   // tiles landed; table and zeroed staging visible
+    DecPrep pr{};
+    if (act) {
+        const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
+        pr = dec_prepare(cur, kTileStep * wid, C, C, lane, tbl, kc);
+        if (lane == 0) xch[wid] = readlane(pr.incl, kOwnLanes - 1u);   // the tile's phase map
+    }
+    __syncthreads();
+    DecLen ln{};
+    u32 oincl = 0u;
+    if (act) {
+        u32 d = 0u;   // token phase entering the tile
+        for (u32 s = 0; s < wid; ++s) d = bfe(xch[s], 8u * d, 8);
+        ln = dec_lengths(pr, d);
+        oincl = wave_scan_incl(ln.nout, 0u, OpAdd());
+        constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+        const bool serial = (__builtin_amdgcn_ballot_w64(ln.serial_lane) & kOwned) != 0ull;
+        u32 tailv = 0u;
+        if (pr.tail) {
+            const uint64_t pfb = __builtin_amdgcn_ballot_w64(ln.PF != 0u) & kOwned;
+            if (pfb) {   // the final token's byte extends to U
+                const u32 jf = (u32)__builtin_ctz(ln.PF | 0x10000u) & 15u;
+                const u32* w = pr.w;
+                const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
+                tailv = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+            }
+        }
+        if (lane == 0) {
+            xch[kW + wid] = readlane(oincl, kOwnLanes - 1u);
+            xch[2 * kW + wid] = serial ? 1u : 0u;
+            xch[3 * kW + wid] = tailv;
+        }
+    }
+    __syncthreads();
+    u32 O = 0u, total = 0u, serial = 0u, tail = 0u;
+    for (u32 s = 0; s < ntiles; ++s) {
+        const u32 c = xch[kW + s];
+        O += s < wid ? c : 0u;
+        total += c;
+        serial |= xch[2 * kW + s];
+        tail |= xch[3 * kW + s];
+    }
+    if (serial || total > U) {   // not encoder output: the exact serial decoder (dec_tile declines)
+        if (wid == 0u) {
+            const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage);
+            if (lane == 0 && status) status[b] = stat;
+        }
+        return;
+    }
+    if (act && lane < kOwnLanes && !(RLE_ABL & 2)) dec_scatter(ln, pr.w, lds_addr(stage) + 2u * (16u + O + oincl - ln.nout));
+    __syncthreads();
+    // output chunk q (bytes [16q, 16q + 16)) = staging chunk q + 1: decoded positions below total,
+    // then the tail byte (zero unless the stream ends in an unbounded token); every chunk holds a
+    // key, so the byte entering chunk q is chunk q - 1's last key (lastb, through LDS across waves)
+    const u32 nq = (U + 15u) >> 4, nthr = kWave * nact, tv = rep4(tail & 0xFFu);
+    for (u32 q0 = 0; q0 < nq; q0 += nthr) {
+        const u32 q = q0 + threadIdx.x;
+        u32x4 a, c;
+        dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u * (q + 1u)), a, c);
+        u32 L[8];
+        dec_fill_scan(a, c, L);
+        if (q < nq) lastb[q] = (L[7] >> 16) & 0xFFu;
+        __syncthreads();
+        if (q < nq) {
+            const u32x4 f = dec_fill_out(L, q ? lastb[q - 1u] : 0u);
+            const u32 fv[4] = {f.x, f.y, f.z, f.w};
+            const u32 rel = 16u * q < total ? total - 16u * q : 0u;
+            u32 ob[4];
+#pragma unroll
+            for (u32 k = 0; k < 4; ++k) {
+                const u32 nb = rel > 4u * k ? (rel - 4u * k < 4u ? rel - 4u * k : 4u) : 0u;
+                const u32 m = lowmask(8u * nb);
+                ob[k] = (fv[k] & m) | (tv & ~m);
+            }
+            if (16u * q + 16u <= U) {
+                vstore(rso, 16u * q, u32x4{ob[0], ob[1], ob[2], ob[3]}, wt != 0u);
+            } else {
+                for (u32 j = 0; 16u * q + j < U; ++j) dst[16u * q + j] = (uint8_t)(ob[j >> 2] >> (8u * (j & 3u)));
+            }
+        }
+    }
+    if (threadIdx.x == 0 && status) status[b] = total < U ? RLE_STATUS_SHORT : RLE_STATUS_OK;
+}
+
+}  // namespace rle
+
+// ================================================================ C-ABI launchers
+namespace {
+uint32_t coop_store_policy(uint32_t n) {
+    // write-through for launches whose output fits in the L2s (rle_kernels.hip store_policy)
+    static const int force = [] {
+        const char* e = getenv("RLE_MI355X_STORE");
+        return !e ? -1 : !strcmp(e, "wt") ? 1 : !strcmp(e, "wb") ? 0 : -1;
+    }();
+    return force >= 0 ? (uint32_t)force : (n <= 4096u ? 1u : 0u);
+}
+// RLE_MI355X_COOP=0 never, =1 always (when the sizes qualify); default: when the whole launch is
+// resident at once (n x waves within kCoopWaves).  Past that the cooperative workgroups run in
+// rounds, each paying a whole buffer's setup chain, and the one-wave kernels are faster
+// (configs[1], 4096 x 4 KiB: decode 21.5 us cooperative vs 13.3 us one-wave; encode 11.9 vs 11.2).
+constexpr uint64_t kCoopWaves = 6144;   // of 8192 wave slots (256 CUs x 32)
+bool coop_enabled(uint32_t n, uint32_t waves) {
+    const char* e = getenv("RLE_MI355X_COOP");   // read per launch: tests switch it in-process
+    const int mode = e ? atoi(e) : -1;
+    return mode == 0 ? false : mode == 1 ? true : (uint64_t)n * waves <= kCoopWaves;
+}
+}  // namespace
+
+// Cooperative launches (include/rle_mi355x.h *_sized): 1 if launched, 0 if the batch does not
+// qualify (the caller then uses the one-wave kernels), < 0 on a launch error.
+extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                                      const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
+                                      uint64_t max_len, void* stream) {
+    if (max_len > rle::kEncStep * rle::kCoopMaxWaves || max_len <= rle::kEncStep) return 0;
+    const uint32_t tiles = (uint32_t)((max_len + rle::kEncStep - 1) / rle::kEncStep);
+    if (!coop_enabled(n, tiles)) return 0;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t wt = coop_store_policy(n);
+    const dim3 g(n);
+#define RLE_ENC_COOP(W)                                                                                         \
+    hipLaunchKernelGGL(rle::enc_coop_kernel<W>, g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, d_in_len, \
+                       (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt)
+    if (tiles <= 2) RLE_ENC_COOP(2);
+    else if (tiles <= 3) RLE_ENC_COOP(3);
+    else if (tiles <= 4) RLE_ENC_COOP(4);
+    else if (tiles <= 6) RLE_ENC_COOP(6);
+    else RLE_ENC_COOP(8);
+#undef RLE_ENC_COOP
+    return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
+}
+
+extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                                      const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap,
+                                      uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint64_t max_out_len,
+                                      void* stream) {
+    if (max_in_len > (uint64_t)rle::kTileStep * rle::kCoopMaxWaves || max_in_len <= rle::kTileStep ||
+        max_out_len > 16384u)
+        return 0;
+    const uint32_t tiles = (uint32_t)((max_in_len + rle::kTileStep - 1) / rle::kTileStep);
+    if (!coop_enabled(n, tiles)) return 0;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t wt = coop_store_policy(n);
+    const dim3 g(n);
+#define RLE_DEC_COOP(W, UM)                                                                                            \
+    hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, d_in_len, \
+                       (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt)
+    if (max_out_len <= 4096u) {
+        if (tiles <= 2) RLE_DEC_COOP(2, 4096);
+        else if (tiles <= 3) RLE_DEC_COOP(3, 4096);
+        else if (tiles <= 5) RLE_DEC_COOP(5, 4096);
+        else RLE_DEC_COOP(8, 4096);
+    } else {
+        if (tiles <= 2) RLE_DEC_COOP(2, 16384);
+        else if (tiles <= 3) RLE_DEC_COOP(3, 16384);
+        else if (tiles <= 5) RLE_DEC_COOP(5, 16384);
+        else RLE_DEC_COOP(8, 16384);
+    }
+#undef RLE_DEC_COOP
+    return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
+}

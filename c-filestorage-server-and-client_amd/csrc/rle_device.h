@@ -387,9 +387,11 @@ struct EncK {
 __device__ __forceinline__ EncK enc_k() {
     return EncK{vconst(0x80808080u), vconst(0x08040201u), vconst(0x80402010u), vconst(0x01010101u)};
 }
+// enc_analyze_bounds: everything but the token masks, which depend on the run entering the tile
+// (enc_tokens).
 template <bool k64>
-__device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, const uint2 look, u32 pos, u32 Ud, u32 Uo, u32 lane,
-                                             u32 prev_top, u32 rs, const EncK& kc) {
+__device__ __forceinline__ EncAn enc_analyze_bounds(const u32x4 cur, const uint2 look, u32 pos, u32 Ud, u32 Uo,
+                                                    u32 lane, u32 prev_top, const EncK& kc) {
     const bool owned = k64 || lane < kOwnLanes;
     EncAn a;
     a.w[0] = cur.x; a.w[1] = cur.y; a.w[2] = cur.z; a.w[3] = cur.w;
@@ -444,19 +446,31 @@ __device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, const uint2 look, 
     const bool every = (__builtin_amdgcn_ballot_w64(B == 0u) & kOwnedMask) == 0ull;
     const u32 incl = every ? lbp : wave_scan_incl(lbp, 0u, OpMax());
     a.incl = incl;
-    const u32 pm = from_prev_lane(incl, 0u);
+    a.T = a.P = 0u;
+    return a;
+}
+// Token masks of an analysed tile, given rs = the start of the run holding the byte before the
+// tile: token starts T (run starts, 9 past a run start, and the continuation of the run entering
+// the lane) and 3-byte tokens P.
+__device__ __forceinline__ void enc_tokens(EncAn& a, u32 rs) {
+    const u32 B = a.B;
+    const u32 pm = from_prev_lane(a.incl, 0u);
     const u32 rsl = pm > rs ? pm : rs;
-    const u32 qin = mod9(p0 - 1u - rsl);   // run phase of byte p0-1 (unused when p0 starts a run)
-
-    // token starts: run starts, 9 past a run start, and the continuation of the run entering
+    const u32 qin = mod9(a.p0 - 1u - rsl);   // run phase of byte p0-1 (unused when p0 starts a run)
     const u32 f1 = (u32)__builtin_ctz(B | 0x10000u);
     u32 t8 = B | (B << 1);
     t8 |= t8 << 2;
     t8 |= t8 << 4;
     t8 |= B << 8;
     const u32 pre = (0x201u << (8u - qin)) & lowmask(f1);
-    a.T = (B | ((B << 9) & ~t8) | pre) & validm;
+    a.T = (B | ((B << 9) & ~t8) | pre) & a.validm;
     a.P = a.T & ~(a.B24 >> 1);   // 3-byte tokens: the run continues past the start
+}
+template <bool k64>
+__device__ __forceinline__ EncAn enc_analyze(const u32x4 cur, const uint2 look, u32 pos, u32 Ud, u32 Uo, u32 lane,
+                                             u32 prev_top, u32 rs, const EncK& kc) {
+    EncAn a = enc_analyze_bounds<k64>(cur, look, pos, Ud, Uo, lane, prev_top, kc);
+    enc_tokens(a, rs);
     return a;
 }
 
@@ -913,6 +927,31 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     return p.tail ? dec_lengths_t<true>(p, d) : dec_lengths_t<false>(p, d);
 }
 
+// The scatter of one lane's decoded positions into the staging (2 bytes per position): endk = the
+// staging byte address of the lane's first decoded position.  u16 per position: the byte, with
+// the start flag (0x80) as the high byte: 0x80vv at a token start, an unflagged 0x00vv (ignored by
+// the fill) anywhere else.
+__device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 endk) {
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 xk_lo = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x05010400u);
+        const u32 xk_hi = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x07030602u);
+        u32 Q = fadd(ln.W[k], fshr<8>(ln.W[k]));
+        Q = fadd(Q, fshr<16>(Q));                        // byte i: decoded bytes of positions >= i
+        Q = Q << 1;                                      // 2 staging bytes per position
+        endk = fadd(endk, fandi<0xFFu>(Q));              // staging address after the dword's output
+        const u32 R = fadd(Q, ln.N02[k]);                // interior positions: one slot further back
+        auto put = [](u32 t, u32 key) {
+            if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
+            else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
+        };
+        put(sub_byte<0>(endk, R), xk_lo);
+        put(sub_byte<1>(endk, R), xk_lo >> 16);
+        put(sub_byte<2>(endk, R), xk_hi);
+        put(sub_byte<3>(endk, R), xk_hi >> 16);
+    }
+}
+
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
                                         u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
                                         DecState& st, const DecK& kc) {
@@ -956,28 +995,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
         }
         // staging byte address after this lane's output (2 B per decoded position)
         u32 endk = lds_addr(stage) + 2u * (16u + rel0 + oincl - done - ln.nout);
-        if (lane < upto && lane >= from && !(RLE_ABL & 2)) {
-#pragma unroll
-            for (u32 k = 0; k < 4; ++k) {
-                // u16 per position: the byte, with the start flag (0x80) as the high byte: 0x80vv at a
-                // token start, an unflagged 0x00vv (ignored by the fill) anywhere else
-                const u32 xk_lo = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x05010400u);
-                const u32 xk_hi = __builtin_amdgcn_perm(ln.S80[k], w[k], 0x07030602u);
-                u32 Q = fadd(ln.W[k], fshr<8>(ln.W[k]));
-                Q = fadd(Q, fshr<16>(Q));                        // byte i: decoded bytes of positions >= i
-                Q = Q << 1;                                      // 2 staging bytes per position
-                endk = fadd(endk, fandi<0xFFu>(Q));              // staging address after the dword's output
-                const u32 R = fadd(Q, ln.N02[k]);                // interior positions: one slot further back
-                auto put = [](u32 t, u32 key) {
-                    if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
-                    else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
-                };
-                put(sub_byte<0>(endk, R), xk_lo);
-                put(sub_byte<1>(endk, R), xk_lo >> 16);
-                put(sub_byte<2>(endk, R), xk_hi);
-                put(sub_byte<3>(endk, R), xk_hi >> 16);
-            }
-        }
+        if (lane < upto && lane >= from && !(RLE_ABL & 2)) dec_scatter(ln, w, endk);
         wave_lds_sync();
         RLE_STAMP(st.sp, 2);   // scatter
 

@@ -273,7 +273,7 @@ bool queue_encode(Ctx* c, const uint8_t* d_src, size_t n) {
     const int erc = n >= kSegEncodeBytes
                         ? rle_encode_batch_device_seg(d_src, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, d_status, 1, n,
                                                       c->d_ws, c->d_ws_cap, c->s)
-                        : rle_encode_batch_device(d_src, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, d_status, 1, c->s);
+                        : rle_encode_batch_device_sized(d_src, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, d_status, 1, n, c->s);
     if (erc != RLE_OK) die("encode launch", hipGetLastError());
     check(hipMemcpyAsync(hm + 3, dm + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
     const bool one_trip = n <= kOneTripBytes;
@@ -321,8 +321,8 @@ void queue_decode(Ctx* c, const uint8_t* d_src, size_t C, uint8_t* d_dst, size_t
     const int drc = C >= kSegDecodeBytes
                         ? rle_decode_batch_device_seg(d_src, dm + 0, dm + 1, d_dst, dm + 2, dm + 3, dm + 4, d_status, 1,
                                                       C, c->d_ws, c->d_ws_cap, c->s)
-                        : rle_decode_batch_device(d_src, dm + 0, dm + 1, d_dst, dm + 2, dm + 3, dm + 4, d_status, 1,
-                                                  c->s);
+                        : rle_decode_batch_device_sized(d_src, dm + 0, dm + 1, d_dst, dm + 2, dm + 3, dm + 4, d_status, 1,
+                                                        C, U, c->s);
     if (drc != RLE_OK) die("decode launch", hipGetLastError());
     check(hipMemcpyAsync(hm + 5, dm + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
 }
@@ -423,8 +423,8 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
     uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
     hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0;
     uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-    if (rle_encode_batch_device(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
-                                reinterpret_cast<uint32_t*>(dw + 4), 1, c->s) != RLE_OK)
+    if (rle_encode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
+                                      reinterpret_cast<uint32_t*>(dw + 4), 1, U, c->s) != RLE_OK)
         die("encode launch", hipGetLastError());
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     const size_t C = hw[3];
@@ -443,8 +443,8 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
     uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
     hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
     uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-    if (rle_decode_batch_device(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
-                                reinterpret_cast<uint32_t*>(dw + 5), 1, c->s) != RLE_OK)
+    if (rle_decode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
+                                      reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, c->s) != RLE_OK)
         die("decode launch", hipGetLastError());
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     const uint32_t st = (uint32_t)hw[5];
@@ -470,8 +470,8 @@ char* compress_small(Ctx* c, const char* data, size_t U, size_t* compressedSize)
     check(hipMemcpyAsync(c->d_in, c->h_in, Ur + kMetaBytes, hipMemcpyHostToDevice, c->s), "H2D");
     uint64_t* dm = reinterpret_cast<uint64_t*>(c->d_in + Ur);
     uint64_t* dmo = reinterpret_cast<uint64_t*>(c->d_out + Cr);   // [C, status]
-    if (rle_encode_batch_device(c->d_in, dm + 0, dm + 1, c->d_out, dm + 2, dmo, reinterpret_cast<uint32_t*>(dmo + 1),
-                                1, c->s) != RLE_OK)
+    if (rle_encode_batch_device_sized(c->d_in, dm + 0, dm + 1, c->d_out, dm + 2, dmo, reinterpret_cast<uint32_t*>(dmo + 1),
+                                      1, U, c->s) != RLE_OK)
         die("encode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_out, c->d_out, Cr + kMetaBytes, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
@@ -493,7 +493,7 @@ void decompress_small(Ctx* c, const char* data, size_t C, size_t U, size_t E, ch
     check(hipMemcpyAsync(c->d_in, c->h_in, Cr + kMetaBytes, hipMemcpyHostToDevice, c->s), "H2D");
     uint64_t* dm = reinterpret_cast<uint64_t*>(c->d_in + Cr);
     uint32_t* d_status = reinterpret_cast<uint32_t*>(c->d_out + Tr);
-    if (rle_decode_batch_device(c->d_in, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, dm + 4, d_status, 1, c->s) !=
+    if (rle_decode_batch_device_sized(c->d_in, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, dm + 4, d_status, 1, C, U, c->s) !=
         RLE_OK)
         die("decode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_out, c->d_out, Tr + kMetaBytes, hipMemcpyDeviceToHost, c->s), "D2H");
@@ -539,14 +539,14 @@ bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* a
     check(hipMemcpyAsync(c->d_in, c->h_in, inBytes, hipMemcpyHostToDevice, c->s), "H2D");
     uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_in + offW);
     uint64_t* res = reinterpret_cast<uint64_t*>(c->d_out + Er);
-    if (rle_decode_batch_device(c->d_in, dw + 0, dw + 1, c->d_mid, dw + 2, dw + 3, dw + 4,
-                                reinterpret_cast<uint32_t*>(res + 2), 1, c->s) != RLE_OK)
+    if (rle_decode_batch_device_sized(c->d_in, dw + 0, dw + 1, c->d_mid, dw + 2, dw + 3, dw + 4,
+                                      reinterpret_cast<uint32_t*>(res + 2), 1, C, U, c->s) != RLE_OK)
         die("decode launch", hipGetLastError());
     if (rle_append_prepare_launch(c->d_mid, U, c->d_in + Cr, reinterpret_cast<unsigned long long*>(dw + 8), res + 3,
                                   c->s) != RLE_OK)
         die("append launch", hipGetLastError());
-    if (rle_encode_batch_device(c->d_in, dw + 5, dw + 6, c->d_out, dw + 7, res + 0, reinterpret_cast<uint32_t*>(res + 1),
-                                1, c->s) != RLE_OK)
+    if (rle_encode_batch_device_sized(c->d_in, dw + 5, dw + 6, c->d_out, dw + 7, res + 0, reinterpret_cast<uint32_t*>(res + 1),
+                                      1, 16 + A, c->s) != RLE_OK)
         die("encode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_out, c->d_out, outBytes, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
@@ -838,8 +838,12 @@ void decompress_n_chunk(Ctx* c, size_t* idx, size_t m, char* const* data, const 
                                                            [&](size_t i) { return compressedSize[i] >= kSegDecodeBytes; }) -
                                      idx)
                           : 0;
-    size_t inLarge = 0;
+    size_t inLarge = 0, maxCs = 0, maxUs = 0;
     for (size_t k = 0; k < mL; ++k) inLarge += round16(compressedSize[idx[k]]);
+    for (size_t k = mL; k < m; ++k) {   // the one-wave launch's sizes (the cooperative kernels' hint)
+        maxCs = std::max(maxCs, compressedSize[idx[k]]);
+        maxUs = std::max(maxUs, uncompressedSize[idx[k]]);
+    }
     // per-file metadata, one pinned block: in_off, in_len, out_off, out_len (m u64 each), status (m u32)
     const size_t metaBytes = 32 * m + 4 * m;
     grow_host(c->h_bm, c->h_bm_cap, metaBytes);
@@ -867,8 +871,8 @@ void decompress_n_chunk(Ctx* c, size_t* idx, size_t m, char* const* data, const 
     if (mL && rle_decode_batch_device_seg(c->d_in, db, db + m, c->d_out, db + 2 * m, db + 3 * m, nullptr, d_status,
                                           (uint32_t)mL, inLarge, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
         die("decode launch", hipGetLastError());
-    if (m > mL && rle_decode_batch_device(c->d_in, db + mL, db + m + mL, c->d_out, db + 2 * m + mL, db + 3 * m + mL,
-                                          nullptr, d_status + mL, (uint32_t)(m - mL), c->s) != RLE_OK)
+    if (m > mL && rle_decode_batch_device_sized(c->d_in, db + mL, db + m + mL, c->d_out, db + 2 * m + mL, db + 3 * m + mL,
+                                                nullptr, d_status + mL, (uint32_t)(m - mL), maxCs, maxUs, c->s) != RLE_OK)
         die("decode launch", hipGetLastError());
     check(hipMemcpyAsync(c->h_out, c->d_out, outTot, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipMemcpyAsync(hb + 4 * m, d_status, 4 * m, hipMemcpyDeviceToHost, c->s), "D2H(status)");

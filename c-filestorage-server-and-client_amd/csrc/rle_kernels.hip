@@ -522,6 +522,41 @@ extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_of
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 
+// Cooperative small-buffer kernels (rle_coop.hip): 1 if launched, 0 if the batch does not qualify.
+extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                                      const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
+                                      uint64_t max_len, void* stream);
+extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                                      const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap,
+                                      uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint64_t max_out_len,
+                                      void* stream);
+
+extern "C" int rle_encode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                             void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                                             uint32_t* d_status, uint32_t n, uint64_t max_in_len, void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
+    if (n > kMaxGrid) return RLE_E_INVAL;
+    const int c = rle_encode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, max_in_len,
+                                         stream);
+    if (c != 0) return c > 0 ? RLE_OK : c;
+    return rle_encode_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, stream);
+}
+
+extern "C" int rle_decode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                             void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                                             const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
+                                             uint64_t max_in_len, uint64_t max_out_len, void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
+    if (n > kMaxGrid) return RLE_E_INVAL;
+    const int c = rle_decode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n,
+                                         max_in_len, max_out_len, stream);
+    if (c != 0) return c > 0 ? RLE_OK : c;
+    return rle_decode_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n,
+                                   stream);
+}
+
 extern "C" int rle_gen_synthetic_device(void* d_out, const uint64_t* d_off, const uint64_t* d_len,
                                         const uint32_t* d_kind, const uint64_t* d_index, uint32_t n, void* stream) {
     if (n == 0) return RLE_OK;

@@ -59,6 +59,11 @@ def lib():
     L.rle_encode_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, vp]
     L.rle_decode_batch_device.restype = ctypes.c_int
     L.rle_decode_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    u64 = ctypes.c_uint64
+    L.rle_encode_batch_device_sized.restype = ctypes.c_int
+    L.rle_encode_batch_device_sized.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u64, vp]
+    L.rle_decode_batch_device_sized.restype = ctypes.c_int
+    L.rle_decode_batch_device_sized.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u64, u64, vp]
     L.rle_seg_workspace_bytes.restype = sz
     L.rle_seg_workspace_bytes.argtypes = [u32, ctypes.c_uint64]
     L.rle_encode_batch_device_seg.restype = ctypes.c_int
@@ -176,20 +181,33 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None):
-    """Batched encode on device tensors (uint8 data; int64 offsets/lengths; int32 status)."""
+def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None, max_len=None):
+    """Batched encode on device tensors (uint8 data; int64 offsets/lengths; int32 status).  With
+    max_len (>= every in_len) the sized entry point runs, which takes the cooperative kernels for
+    batches of small buffers."""
     n = in_off.numel()
-    rc = lib().rle_encode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
-                                       _ptr(out_len), _ptr(status), n, _stream_ptr(stream))
+    if max_len is None:
+        rc = lib().rle_encode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                           _ptr(out_len), _ptr(status), n, _stream_ptr(stream))
+    else:
+        rc = lib().rle_encode_batch_device_sized(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                                 _ptr(out_len), _ptr(status), n, int(max_len), _stream_ptr(stream))
     if rc != RLE_OK:
         raise RLEError(f"rle_encode_batch_device failed: {rc}")
 
 
-def decode_batch(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, status=None, stream=None):
-    """Batched decode on device tensors."""
+def decode_batch(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, status=None, stream=None,
+                 max_in_len=None, max_out_len=None):
+    """Batched decode on device tensors.  With max_in_len / max_out_len (>= every in_len / out_len)
+    the sized entry point runs (cooperative kernels for batches of small buffers)."""
     n = in_off.numel()
-    rc = lib().rle_decode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
-                                       _ptr(out_len), _ptr(out_cap), _ptr(status), n, _stream_ptr(stream))
+    if max_in_len is None or max_out_len is None:
+        rc = lib().rle_decode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                           _ptr(out_len), _ptr(out_cap), _ptr(status), n, _stream_ptr(stream))
+    else:
+        rc = lib().rle_decode_batch_device_sized(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                                 _ptr(out_len), _ptr(out_cap), _ptr(status), n, int(max_in_len),
+                                                 int(max_out_len), _stream_ptr(stream))
     if rc != RLE_OK:
         raise RLEError(f"rle_decode_batch_device failed: {rc}")
 

@@ -66,6 +66,21 @@ int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const ui
                             void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
                             const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n, void* stream);
 
+/* The same two launches with the batch's largest sizes known on the host (max_in_len >= every
+ * d_in_len[i]; decode: max_out_len >= every d_out_len[i]).  Few small buffers (encode:
+ * max_in_len <= 8 KiB; decode: max_in_len <= 8064 and max_out_len <= 16 KiB; and at most about
+ * 6144 waves in all, one per tile) then run the cooperative kernels, one workgroup per buffer
+ * and one wave per tile, so a buffer's tiles run side by side instead of one after another (a
+ * single file, a small readN).  Other batches (or RLE_MI355X_COOP=0) take the kernels above.
+ * Output and status are the same bytes. */
+int rle_encode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                  void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                                  uint32_t* d_status, uint32_t n, uint64_t max_in_len, void* stream);
+int rle_decode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                  void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                                  const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
+                                  uint64_t max_in_len, uint64_t max_out_len, void* stream);
+
 /* Synthetic batch generator: xorshift64 (13,7,17), state seed
  * 0x9E3779B97F4A7C15 + index, one step per byte; kind 0 zero, 1 random, 2 runs50,
  * 3 runs90, 4 pairs.  d_kind / d_index may be NULL (kind 1, index = i). */

@@ -1,0 +1,114 @@
+"""GPU parity of the cooperative small-buffer kernels (csrc/rle_coop.hip: one workgroup per buffer,
+one wave per tile), reached through the sized entry points of include/rle_mi355x.h, against the
+oracle and the compiled reference's golden vectors.  Bit-exact everywhere, slots poisoned.
+
+The size hints choose the kernel; a hint smaller than a buffer (allowed only here, to reach the
+path) sends that buffer to the workgroup's one-wave fallback, so both paths of the kernel run."""
+import numpy as np
+import pytest
+
+import rle_oracle as O
+from test_gpu_parity import gpu_decode, gpu_encode
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _always_coop():
+    # the launcher's default takes the cooperative kernels only for launches resident at once;
+    # these tests run them for every batch (RLE_MI355X_COOP is read at each launch)
+    import os
+    old = os.environ.get("RLE_MI355X_COOP")
+    os.environ["RLE_MI355X_COOP"] = "1"
+    yield
+    if old is None:
+        del os.environ["RLE_MI355X_COOP"]
+    else:
+        os.environ["RLE_MI355X_COOP"] = old
+
+
+def _hints(xs, ys):
+    return max(len(x) for x in xs), max(len(y) for y in ys), max(len(x) for x in xs)
+
+
+def coop_parity(xs, enc_hint=None, dec_hints=None):
+    """Encode with the sized entry point, compare with the oracle, decode the oracle's streams with
+    the sized entry point, compare with the input."""
+    refs = [O.encode(x) for x in xs]
+    mx = max(1, max(len(x) for x in xs))
+    ys, st = gpu_encode(xs, max_len=enc_hint if enc_hint is not None else mx)
+    assert (st == 0).all()
+    bad = [i for i in range(len(xs)) if ys[i] != refs[i]]
+    assert not bad, (len(bad), bad[:3], [len(xs[i]) for i in bad[:3]])
+    mi = max(1, max(len(y) for y in refs))
+    hi, ho = dec_hints if dec_hints is not None else (mi, mx)
+    dec, st = gpu_decode(refs, [len(x) for x in xs], max_in_len=hi, max_out_len=ho)
+    bad = [i for i in range(len(xs)) if dec[i] != xs[i]]
+    assert not bad, (len(bad), bad[:3], [len(xs[i]) for i in bad[:3]])
+    assert ((st & 0xFF) == 0).all()
+
+
+def test_config1_shape():
+    # BASELINE configs[1]: 4096 x 4 KiB random / zero
+    coop_parity([O.gen(1 if i % 2 == 0 else 0, i, 4096) for i in range(4096)])
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_every_kind_and_small_size(kind):
+    sizes = [0, 1, 2, 15, 16, 17, 1007, 1008, 1009, 1023, 1024, 1025, 2016, 2017, 2048, 2049, 3024, 3072, 4095,
+             4096, 4097, 5000, 6143, 6144, 7000, 8191, 8192]
+    coop_parity([O.gen(kind, 7 * kind + i, s) for i, s in enumerate(sizes)])
+
+
+def test_runs_and_digits_across_tile_edges():
+    # runs that end or cross a tile edge (1008 k decode, 1024 k encode) by 1..10 bytes, digit bytes
+    xs = []
+    for k in range(1, 8):
+        for edge in (1008 * k, 1024 * k):
+            for r in (1, 2, 3, 8, 9, 10, 11, 18, 19):
+                for side in (-1, 0, 1):
+                    n = min(8192, edge + 40)
+                    x = bytearray(O.gen(1, 97 * edge + r, n))
+                    lo = max(0, edge - r if side <= 0 else edge)
+                    hi = min(n, edge + r if side >= 0 else edge)
+                    x[lo:hi] = (b"7" if r % 2 else b"\0") * (hi - lo)
+                    xs.append(bytes(x))
+    rng = np.random.default_rng(17)
+    for i in range(400):
+        s = int(rng.integers(900, 8192))
+        alpha = np.frombuffer(rng.choice([b"a0123456789", b"\0\x01", b"33", b"ab", b"99"]), np.uint8)
+        xs.append(np.repeat(rng.choice(alpha, size=s), rng.integers(1, 22, size=s))[:s].tobytes())
+    coop_parity(xs)
+
+
+def test_golden_vectors(vectors):
+    cases = [v for g in ("kat", "edge", "ladder", "fuzz") for v in vectors[g]]
+    xs = [bytes.fromhex(v["in"]) for v in cases]
+    ys = [bytes.fromhex(v["out"]) for v in cases]
+    got, st = gpu_encode(xs, max_len=max(len(x) for x in xs))
+    assert got == ys and (st == 0).all()
+    dec, st = gpu_decode(ys, [len(x) for x in xs], max_in_len=max(len(y) for y in ys),
+                         max_out_len=max(len(x) for x in xs))
+    assert dec == xs and ((st & 0xFF) == 0).all()
+
+
+def test_invalid_streams_and_overflow(vectors):
+    # streams the tiled path declines take the exact serial decoder inside the cooperative kernel
+    cases = vectors["invalid_decode"]
+    streams = [bytes.fromhex(v["in"]) for v in cases]
+    us = [v["U"] for v in cases]
+    caps = [v["U"] + v["E"] for v in cases]
+    dec, st = gpu_decode(streams, us, caps, poison=False, max_in_len=max(2048, max(len(s) for s in streams)),
+                         max_out_len=max(us))
+    bad = [i for i in range(len(cases)) if dec[i] != bytes.fromhex(cases[i]["out"])]
+    assert not bad, (len(bad), cases[bad[0]], dec[bad[0]].hex())
+    dec, st = gpu_decode([b"aa9" * 3, b"aa9", b"b" * 1500], [2, 9, 1500], [2, 9, 1500], max_in_len=1500,
+                         max_out_len=1500)
+    assert st[0] & 1 and dec[0] == b"aa" and st[1] == 0 and dec[1] == b"a" * 9 and dec[2] == b"b" * 1500
+
+
+def test_hints_smaller_than_buffers_fall_back():
+    # buffers past the kernel's tiles (or, decode, its staging) are walked by wave 0 alone
+    xs = [O.gen(i % 5, 300 + i, s) for i, s in enumerate([3000, 9000, 20000, 70000, 1500, 100, 4096, 16385])]
+    coop_parity(xs, enc_hint=2048, dec_hints=(2016, 4096))
+    coop_parity(xs, enc_hint=8192, dec_hints=(8064, 16384))

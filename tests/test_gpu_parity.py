@@ -26,9 +26,10 @@ def _i64(vals):
     return torch.tensor(np.asarray(vals, dtype=np.int64), device=DEV)
 
 
-def gpu_encode(bufs, seg=False):
-    """Encode a list of byte strings in ONE batched launch (seg: the segmented multi-wave form);
-    returns (outputs, status)."""
+def gpu_encode(bufs, seg=False, max_len=None):
+    """Encode a list of byte strings in ONE batched launch (seg: the segmented multi-wave form;
+    max_len: the sized entry point with that hint, which picks the cooperative kernels for small
+    buffers); returns (outputs, status)."""
     n = len(bufs)
     sizes = [len(b) for b in bufs]
     in_offs, in_total = R.layout(sizes)
@@ -40,8 +41,11 @@ def gpu_encode(bufs, seg=False):
     d_out = torch.full((out_total + 16,), POISON, dtype=torch.uint8, device=DEV)
     out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
-    (R.encode_batch_seg if seg else R.encode_batch)(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs),
-                                                    out_len, status)
+    if max_len is not None:
+        R.encode_batch(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status, max_len=max_len)
+    else:
+        (R.encode_batch_seg if seg else R.encode_batch)(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs),
+                                                        out_len, status)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
     lens = out_len.cpu().numpy()
@@ -54,7 +58,7 @@ def gpu_encode(bufs, seg=False):
     return res, status.cpu().numpy()
 
 
-def gpu_decode(streams, usizes, caps=None, poison=True, seg=False):
+def gpu_decode(streams, usizes, caps=None, poison=True, seg=False, max_in_len=None, max_out_len=None):
     n = len(streams)
     caps = caps if caps is not None else list(usizes)
     in_offs, in_total = R.layout([len(s) for s in streams])
@@ -65,8 +69,12 @@ def gpu_decode(streams, usizes, caps=None, poison=True, seg=False):
     d_in = torch.from_numpy(host).to(DEV)
     d_out = torch.full((out_total + 16,), POISON if poison else 0, dtype=torch.uint8, device=DEV)
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
-    (R.decode_batch_seg if seg else R.decode_batch)(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out,
-                                                    _i64(out_offs), _i64(usizes), _i64(caps), status)
+    if max_in_len is not None:
+        R.decode_batch(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out, _i64(out_offs), _i64(usizes),
+                       _i64(caps), status, max_in_len=max_in_len, max_out_len=max_out_len)
+    else:
+        (R.decode_batch_seg if seg else R.decode_batch)(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out,
+                                                        _i64(out_offs), _i64(usizes), _i64(caps), status)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
     res = [out[o:o + c].tobytes() for o, c in zip(out_offs, caps)]

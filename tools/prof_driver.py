@@ -22,7 +22,7 @@ B = bench.Batch(bench.WORKLOADS[a.workload], 0, 1, torch.device("cuda", 0))
 B.seg = a.seg
 s = torch.cuda.current_stream()
 B.encode(s)
-torch.cuda.synchronize()
+B.calibrate()
 for _ in range(a.reps):
     B.encode(s)
 for _ in range(a.reps):
