@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <errno.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -105,6 +106,10 @@ constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes =
 // RLE_MI355X_STAGE_CAP=<bytes> overrides it (tests use small caps to cover the chunking).
 size_t g_stage_cap = 32u << 20;
 
+// RLE_MI355X_FAIL_ALLOC_ABOVE=<bytes> (tests only): staging / device allocations larger than that
+// fail as if memory were exhausted, so the allocation-failure paths can be exercised.
+size_t g_fail_above = SIZE_MAX;
+
 struct Ctx {
     int dev = 0;
     uint8_t* h_zc = nullptr;                         // mapped pinned buffer of the zero-copy calls
@@ -175,6 +180,7 @@ void init_once() {
         if (!strcmp(e, "pinned")) g_staging = Staging::Pinned;
         else if (!strcmp(e, "pipe")) g_staging = Staging::Pipe;
     }
+    if (const char* e = getenv("RLE_MI355X_FAIL_ALLOC_ABOVE")) g_fail_above = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_STAGE_CAP")) {
         const long long v = atoll(e);
         if (v >= 16) g_stage_cap = (size_t)v;
@@ -230,7 +236,7 @@ void grow_host(uint8_t*& p, size_t& cap, size_t need) {
     if (p) check(hipHostFree(p), "hipHostFree");
     p = nullptr;
     cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess) {
+    if (n > g_fail_above || hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
         throw std::bad_alloc();
@@ -245,7 +251,7 @@ void grow_dev(uint8_t*& p, size_t& cap, size_t need) {
     if (p) check(hipFree(p), "hipFree");
     p = nullptr;
     cap = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&p), n) != hipSuccess) {
+    if (n > g_fail_above || hipMalloc(reinterpret_cast<void**>(&p), n) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
         throw std::bad_alloc();

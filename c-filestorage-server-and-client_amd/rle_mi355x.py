@@ -51,7 +51,7 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RLEError(f"{LIB_PATH} is missing: the HIP codec has not been built")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH, use_errno=True)   # errno of the drop-in calls (ENOMEM, EFBIG, EINVAL)
     vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
     L.rle_max_compressed_size.restype = sz
     L.rle_max_compressed_size.argtypes = [sz]

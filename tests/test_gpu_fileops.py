@@ -180,3 +180,45 @@ def test_fileops_concurrent_threads():
     for x in th:
         x.join()
     assert not errors, errors[:5]
+
+
+def test_allocation_failure_returns_null_enomem():
+    """An allocation the drop-in cannot make returns what the reference's failed calloc gives its
+    callers (NULL / -1, errno = ENOMEM; src/filesystemApi.c:598-600, 681-684) instead of aborting
+    the server, and the thread's later calls work.  Allocations past 1 MiB are made to fail
+    (RLE_MI355X_FAIL_ALLOC_ABOVE, read at library init: a fresh process)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import ctypes, errno, sys
+sys.path[:0] = sys.argv[1:3]
+import rle_mi355x as R, rle_oracle as O
+L = ctypes.CDLL(R.LIB_PATH, use_errno=True)
+L.RLEcompress.restype = ctypes.c_void_p
+L.RLEcompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+L.RLEdecompress.restype = ctypes.c_void_p
+L.RLEdecompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
+big = O.gen(1, 1, 3 << 20)
+c = ctypes.c_size_t(99)
+ctypes.set_errno(0)
+assert not L.RLEcompress(big, len(big), ctypes.byref(c)) and c.value == 0 and ctypes.get_errno() == errno.ENOMEM
+y = O.encode(big)
+ctypes.set_errno(0)
+assert not L.RLEdecompress(y, len(y), len(big), 0) and ctypes.get_errno() == errno.ENOMEM
+xs = [O.gen(2, 7, 2 << 20), O.gen(0, 8, 5000)]
+try:
+    R.decompress_n([O.encode(x) for x in xs], [len(x) for x in xs])
+    raise SystemExit("readN did not fail")
+except R.RLEError as e:
+    assert "errno %d" % errno.ENOMEM in str(e), e
+small = O.gen(3, 9, 40000)
+assert R.compress(small) == O.encode(small) and R.decompress(O.encode(small), len(small)) == small
+print("ok")
+'''
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, RLE_MI355X_FAIL_ALLOC_ABOVE=str(1 << 20))
+    r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "c-filestorage-server-and-client_amd"),
+                        os.path.join(root, "oracle")], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout[-1000:], r.stderr[-2000:])
