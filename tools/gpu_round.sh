@@ -9,6 +9,9 @@ mkdir -p $O
 timeout -k 10 900 python -u -m pytest $R/tests -m gpu -v -rA --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/status
 case $rc in 124|134|137|139) exit $rc;; esac
+timeout -k 10 300 python -u -m pytest $R/tests/test_e2e_server.py -m gpu -s -q --timeout 240 --timeout-method thread > $O/e2e.log 2>&1
+rc=$?; echo "e2e rc=$rc" >> $O/status
+case $rc in 124|134|137|139) exit $rc;; esac
 timeout -k 10 400 python $R/bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc" >> $O/status
 case $rc in 124|134|137|139) exit $rc;; esac
