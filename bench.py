@@ -284,6 +284,33 @@ def main():
                 "unit": "GB/s", "frac": round(kern[dom]["GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "alg_bytes_per_launch": alg, "copy_ceiling": copy_ceiling(B, alg, reps, stream)}
 
+    # Informational, not `value`: the same round trips with two batches in flight on two streams, as
+    # the drop-in runs when the server's worker threads (one HIP stream each) call it concurrently.
+    conc = None
+    if rank == 0 and world == 1 and B.u_bytes <= (256 << 20) and args.steps > 0:
+        B2 = Batch(wl, rank, world, dev)
+        B2.encode(stream)
+        B2.calibrate()
+        ss = [stream, torch.cuda.Stream(device=dev)]
+        pair = [B, B2]
+        for k in range(4):
+            pair[k % 2].encode(ss[k % 2])
+            pair[k % 2].decode(ss[k % 2])
+        torch.cuda.synchronize()
+        t0c = time.perf_counter()
+        for k in range(2 * args.steps):
+            pair[k % 2].encode(ss[k % 2])
+            pair[k % 2].decode(ss[k % 2])
+        torch.cuda.synchronize()
+        dtc = time.perf_counter() - t0c
+        conc = {"streams": 2, "value": round(B.u_bytes * 2 * args.steps / dtc / GIB, 3), "unit": "GiB/s",
+                "us_per_roundtrip": round(dtc / (2 * args.steps) * 1e6, 3),
+                "verified": bool(torch.equal(B2.d_out, B2.d_in)),
+                "note": "two independent batches, each round trip on its own stream (the drop-in's per-thread "
+                        "streams); `value` is one batch after another on one stream"}
+        del B2
+        torch.cuda.empty_cache()
+
     north = None
     if rank == 0 and world == 1 and not args.no_north_star and args.workload != "dec64k":
         del B
@@ -329,7 +356,7 @@ def main():
                           "parallelism": f"shard round-robin over {world} GPU(s)" +
                                          (", RCCL all-gather of sizes" if world > 1 else "")},
                "verified_bit_exact_roundtrip": ok, "kernels": kern, "roofline": roofline, "cpu_baseline": cpu,
-               "north_star_dec64k": north}
+               "north_star_dec64k": north, "concurrent_streams": conc}
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
