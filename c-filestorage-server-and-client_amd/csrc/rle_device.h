@@ -952,13 +952,131 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
     }
 }
 
+// ---------------------------------------------------------------- literal tiles (the fast path)
+// A tile whose tokens are all 1-byte literals or 3-byte pairs "vv2" decodes to its own bytes with
+// the count digits deleted: position j is kept unless it is a pair's digit, or lies before the
+// tile's first token start (the previous tile's token, decoded there).  A pair started at the
+// tile's last owned position keeps its second byte, lane 63's position 0 (the lookahead), so each
+// tile's output is still exactly the tokens that start in it.  When every owned lane loses at most
+// 2 positions, lane l's output is its 16 bytes with <= 2 removed (one LUT-selected v_perm per
+// dword), stored with one 16-byte store at its output offset, which need not be aligned: the
+// lane's 14..16 bytes are followed by the next lane's first bytes, so the bytes two lanes store
+// twice are equal.  The last lane's store reaches <= 16 bytes past the tile's output; the next
+// tile's (or the finish's) stores, issued later by the same wave, overwrite them.  No staging, no
+// scatter, no fill: random and text-like data decode with about half the VALU work.
+#ifndef RLE_DEC_FAST
+#define RLE_DEC_FAST 1
+#endif
+constexpr u32 kNotFast = 0xFFFFFFFEu;
+// Compaction selectors: entry 17 t1 + t2 (a lane's deleted positions t1 < t2, 16 = none), dword q:
+// the v_perm selector taking output bytes 4q..4q+3 from (y[q+1]:y[q]) once t1, t2 are removed.
+constexpr u32 kCompactEntries = 17u * 17u;
+struct DecCompactLut {
+    u32 s[kCompactEntries * 4u];
+};
+constexpr DecCompactLut make_compact_lut() {
+    DecCompactLut t{};
+    for (u32 t1 = 0; t1 <= 16u; ++t1)
+        for (u32 t2 = 0; t2 <= 16u; ++t2)
+            for (u32 q = 0; q < 4u; ++q) {
+                u32 sel = 0;
+                for (u32 b = 0; b < 4u; ++b) {
+                    const u32 m = 4u * q + b;
+                    const u32 s = m + ((t1 < 16u && m >= t1) ? 1u : 0u) + ((t2 < 16u && t2 > t1 && m + 1u >= t2) ? 1u : 0u);
+                    const u32 v = s - 4u * q;
+                    sel |= (v > 7u ? 7u : v) << (8u * b);
+                }
+                t.s[(17u * t1 + t2) * 4u + q] = sel;
+            }
+    return t;
+}
+static __constant__ DecCompactLut kCompactLut = make_compact_lut();
+
+// Returns the store instructions issued, or kNotFast (nothing done: the general path decodes the
+// tile).  Not for tail tiles (pr.tail) nor a segment's first chunk (st.head).
+__device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const u32x4* clut, uint8_t* stage,
+                                             u32x4 rso, u32 U, DecState& st, const DecK& kc) {
+    constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+    const u32* w = pr.w;
+    const u32 NE16 = (pr.xa >> 7) | (pr.xb << 1);
+    // cheap reject first (runs): at most 2 equal neighbours per owned lane
+    if (__builtin_amdgcn_ballot_w64(__builtin_popcount(~NE16 & 0xFFFFu) > 2) & kOwned) return kNotFast;
+    const u32 dl = bfe(pr.excl, 8u * st.d, 8);
+    const u32 mid = __builtin_amdgcn_perm(0u, pr.ta.y, 0x0C0C0C00u | dl);
+    const u32 sa = __builtin_amdgcn_perm(0u, pr.ta.x, 0x0C0C0C00u | dl);
+    const u32 sb = __builtin_amdgcn_perm(0u, pr.tb.x, 0x0C0C0C00u | mid);
+    const u32 P16 = (sa | (sb << 8)) & ~NE16;   // pair starts (bits 0..15)
+    // every pair's count digit (position j + 2) is '2'
+    const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
+                       alignbyte(pr.la, w[3], 2)};
+    u32 nz[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 t = dg[k] ^ 0x32323232u;
+        nz[k] = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80);
+    }
+    const u32 za = __builtin_amdgcn_udot4(nz[1], kc.C2, __builtin_amdgcn_udot4(nz[0], kc.C1, 0u, false), false);
+    const u32 zb = __builtin_amdgcn_udot4(nz[3], kc.C2, __builtin_amdgcn_udot4(nz[2], kc.C1, 0u, false), false);
+    const u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
+    // deleted positions: digits of pairs started in this lane or (bits 14, 15) the lane before, and
+    // in lane 0 the tile's first d positions; lane 63 keeps only a pair's second byte at position 0
+    const u32 prevP = from_prev_lane(P16, 0u);
+    u32 del = ((P16 << 2) | (prevP >> 14)) & 0xFFFFu;
+    if (lane == 0u) del |= lowmask(st.d);
+    const u32 K = lane < kOwnLanes ? (~del & 0xFFFFu) : ((prevP >> 15) & 1u);
+    const u32 kept = (u32)__builtin_popcount(K);
+    const bool reject = (P16 & NZ16) != 0u || kept < 14u;
+    const u32 oincl = wave_scan_incl(kept, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, kWave - 1u);
+    if ((__builtin_amdgcn_ballot_w64(reject) & kOwned) || st.out_pos + ttot + 16u > U) return kNotFast;
+
+    u32 rounds = 0;
+    const u32 rel0 = st.out_pos - st.flushed;
+    if (rel0) {   // a general tile's partial chunk: store it (its bytes past rel0 are rewritten below)
+        u32x4 a, b;
+        dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), a, b);
+        u32 L[8];
+        dec_fill_scan(a, b, L);
+        vstore(rso, lane == 0u ? st.flushed : kOOB, dec_fill_out(L, st.fillc), st.wt);
+        wave_lds_sync();
+        if (lane < 8u)
+            *reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane)) = 0u;
+        wave_lds_sync();
+        rounds = 1;
+    }
+    const u32 dm = lane < kOwnLanes ? del : 0u;
+    const u32 t1 = (u32)__builtin_ctz(dm | 0x10000u);
+    const u32 t2 = (u32)__builtin_ctz((dm & (dm - 1u)) | 0x10000u);
+    const u32x4 sel = clut[17u * t1 + t2];
+    u32x4 o;
+    o.x = __builtin_amdgcn_perm(w[1], w[0], sel.x);
+    o.y = __builtin_amdgcn_perm(w[2], w[1], sel.y);
+    o.z = __builtin_amdgcn_perm(w[3], w[2], sel.z);
+    const u32 c3 = __builtin_amdgcn_perm(w[3], w[3], sel.w);
+    // bytes kept..15 of the store: the next lane's first bytes (kept >= 14 on owned lanes)
+    const u32 n0 = from_next_lane(o.x, 0u);
+    const u32 s3 = kept >= 16u ? 0x03020100u : kept == 15u ? 0x04020100u : 0x05040100u;
+    o.w = lane < kOwnLanes ? __builtin_amdgcn_perm(n0, c3, s3) : c3;
+    vstore(rso, kept ? st.out_pos + oincl - kept : kOOB, o, st.wt);
+    st.out_pos += ttot;
+    st.flushed = st.out_pos;
+    st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
+    st.prev = readlane(w[3], kOwnLanes - 1u);
+    return rounds + 1u;
+}
+
+template <bool kFast = false>
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
                                         u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
-                                        DecState& st, const DecK& kc) {
+                                        DecState& st, const DecK& kc, const u32x4* clut = nullptr) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
     const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
+    if (kFast && RLE_DEC_FAST && !pr.tail && !st.head) {
+        const u32 r = dec_tile_fast(pr, lane, clut, stage, rso, U, st, kc);
+        if (r != kNotFast) return r;
+    }
     const DecLen ln = dec_lengths(pr, st.d);
     const u32* w = pr.w;
     const u32 oincl = wave_scan_incl(ln.nout, 0u, OpAdd());

@@ -271,6 +271,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kDecStage];
     __shared__ DecEntry tbl[256];
+    __shared__ u32x4 clut[kCompactEntries];
 #ifdef RLE_LDS_PAD   // occupancy experiments only
     __shared__ uint8_t ldspad[RLE_LDS_PAD];
     if (threadIdx.x == 0) ((volatile uint8_t*)ldspad)[0] = 0;
@@ -285,6 +286,14 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     DecEntry te[kTblPer];
 #pragma unroll
     for (u32 i = 0; i < kTblPer; ++i) te[i] = dec_entry_from(kDecTable.e[(threadIdx.x + i * kDecBlock) & 255u]);
+    constexpr u32 kLutPer = (kCompactEntries + kDecBlock - 1u) / kDecBlock;
+    u32x4 ce[kLutPer];
+#pragma unroll
+    for (u32 i = 0; i < kLutPer; ++i) {
+        const u32 e = threadIdx.x + i * kDecBlock;
+        const u32* s = &kCompactLut.s[4u * (e < kCompactEntries ? e : 0u)];
+        ce[i] = u32x4{s[0], s[1], s[2], s[3]};
+    }
     // with an issue order, workgroups take its ranks in dispatch order (the heavy buffers first,
     // spread over every XCD); else each XCD takes a contiguous slice of the batch
     u32 b;
@@ -312,6 +321,9 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
 #pragma unroll
     for (u32 i = 0; i < kTblPer; ++i) tbl[(threadIdx.x + i * kDecBlock) & 255u] = te[i];
+#pragma unroll
+    for (u32 i = 0; i < kLutPer; ++i)
+        if (threadIdx.x + i * kDecBlock < kCompactEntries) clut[threadIdx.x + i * kDecBlock] = ce[i];
     stagger();
     walk_prime(rsi, 0u, ntiles, lane, slots);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
@@ -336,7 +348,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             rsi, 0u, ntiles, lane, slots,
             [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 tl_mark(b, 2u + t, lane);
-                return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc);
+                return dec_tile<true>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
             },
             true);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
