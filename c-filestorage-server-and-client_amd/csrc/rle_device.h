@@ -992,21 +992,35 @@ constexpr DecCompactLut make_compact_lut() {
 }
 static __constant__ DecCompactLut kCompactLut = make_compact_lut();
 
+// One 4-byte store (buffer_store_dword; offsets need not be aligned).
+__device__ __forceinline__ void vstore4(u32x4 rs, u32 voff, u32 v, bool wt) {
+    if (wt)
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+    else
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+
 // Returns the store instructions issued, or kNotFast (nothing done: the general path decodes the
-// tile).  Not for tail tiles (pr.tail) nor a segment's first chunk (st.head).
+// tile).  Not for a segment's first chunk (st.head), nor with Co < C (one-wave walks only).
+// kTail (pr.tail): positions past C are neither starts nor kept, a pair whose digit lies past C
+// (the stream's final unbounded token) declines, and since the range check drops a store's dwords
+// that are not wholly below U (tools/probes/range_clip_probe.hip), the tile's last 4 output bytes
+// are stored again as one dword ending at its output end.
+template <bool kTail>
 __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const u32x4* clut, uint8_t* stage,
                                              u32x4 rso, u32 U, DecState& st, const DecK& kc) {
     constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
     const u32* w = pr.w;
+    const u32 lim = kTail ? lowmask(pr.left < 16u ? pr.left : 16u) : 0xFFFFu;   // positions below C
     const u32 NE16 = (pr.xa >> 7) | (pr.xb << 1);
     // cheap reject first (runs): at most 2 equal neighbours per owned lane
-    if (__builtin_amdgcn_ballot_w64(__builtin_popcount(~NE16 & 0xFFFFu) > 2) & kOwned) return kNotFast;
+    if (__builtin_amdgcn_ballot_w64(__builtin_popcount(~NE16 & lim) > 2) & kOwned) return kNotFast;
     const u32 dl = bfe(pr.excl, 8u * st.d, 8);
     const u32 mid = __builtin_amdgcn_perm(0u, pr.ta.y, 0x0C0C0C00u | dl);
     const u32 sa = __builtin_amdgcn_perm(0u, pr.ta.x, 0x0C0C0C00u | dl);
     const u32 sb = __builtin_amdgcn_perm(0u, pr.tb.x, 0x0C0C0C00u | mid);
-    const u32 P16 = (sa | (sb << 8)) & ~NE16;   // pair starts (bits 0..15)
-    // every pair's count digit (position j + 2) is '2'
+    const u32 P16 = (sa | (sb << 8)) & ~NE16 & lim;   // pair starts (bits 0..15)
+    // every pair's count digit (position j + 2) is '2' (and, in a tail tile, lies below C)
     const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
                        alignbyte(pr.la, w[3], 2)};
     u32 nz[4];
@@ -1017,18 +1031,20 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     }
     const u32 za = __builtin_amdgcn_udot4(nz[1], kc.C2, __builtin_amdgcn_udot4(nz[0], kc.C1, 0u, false), false);
     const u32 zb = __builtin_amdgcn_udot4(nz[3], kc.C2, __builtin_amdgcn_udot4(nz[2], kc.C1, 0u, false), false);
-    const u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
+    u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
+    if (kTail) NZ16 |= ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2);   // ... or lies past C
     // deleted positions: digits of pairs started in this lane or (bits 14, 15) the lane before, and
     // in lane 0 the tile's first d positions; lane 63 keeps only a pair's second byte at position 0
     const u32 prevP = from_prev_lane(P16, 0u);
-    u32 del = ((P16 << 2) | (prevP >> 14)) & 0xFFFFu;
-    if (lane == 0u) del |= lowmask(st.d);
-    const u32 K = lane < kOwnLanes ? (~del & 0xFFFFu) : ((prevP >> 15) & 1u);
+    u32 del = ((P16 << 2) | (prevP >> 14)) & lim;
+    if (lane == 0u) del |= lowmask(st.d) & lim;
+    const u32 K = lane < kOwnLanes ? (~del & lim) : ((prevP >> 15) & 1u);
     const u32 kept = (u32)__builtin_popcount(K);
-    const bool reject = (P16 & NZ16) != 0u || kept < 14u;
+    const bool reject = (P16 & NZ16) != 0u || __builtin_popcount(del) > 2;
     const u32 oincl = wave_scan_incl(kept, 0u, OpAdd());
     const u32 ttot = readlane(oincl, kWave - 1u);
-    if ((__builtin_amdgcn_ballot_w64(reject) & kOwned) || st.out_pos + ttot + 16u > U) return kNotFast;
+    if (__builtin_amdgcn_ballot_w64(reject) & kOwned) return kNotFast;
+    if (kTail ? (ttot < 4u || st.out_pos + ttot > U) : st.out_pos + ttot + 16u > U) return kNotFast;
 
     u32 rounds = 0;
     const u32 rel0 = st.out_pos - st.flushed;
@@ -1053,11 +1069,26 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     o.y = __builtin_amdgcn_perm(w[2], w[1], sel.y);
     o.z = __builtin_amdgcn_perm(w[3], w[2], sel.z);
     const u32 c3 = __builtin_amdgcn_perm(w[3], w[3], sel.w);
-    // bytes kept..15 of the store: the next lane's first bytes (kept >= 14 on owned lanes)
+    // bytes kept..15 of the store: the next lane's first bytes (kept >= 14 on full owned lanes;
+    // fewer only where the output ends)
     const u32 n0 = from_next_lane(o.x, 0u);
     const u32 s3 = kept >= 16u ? 0x03020100u : kept == 15u ? 0x04020100u : 0x05040100u;
     o.w = lane < kOwnLanes ? __builtin_amdgcn_perm(n0, c3, s3) : c3;
     vstore(rso, kept ? st.out_pos + oincl - kept : kOOB, o, st.wt);
+    if (kTail) {
+        // the last 4 bytes of each lane's output: from its own bytes, or with fewer than 4 the
+        // previous (full) lane's last bytes and its own
+        const u32 s = kept - 4u, qd = s >> 2;
+        const u32 lo = qd == 0u ? o.x : qd == 1u ? o.y : qd == 2u ? o.z : o.w;
+        const u32 hi = qd == 0u ? o.y : qd == 1u ? o.z : o.w;
+        const u32 T4 = alignbyte(hi, lo, s & 3u);
+        const u32 Tp = from_prev_lane(T4, 0u);
+        const u32 T = kept >= 4u ? T4 : alignbyte(o.x, Tp, kept);
+        const uint64_t has = __builtin_amdgcn_ballot_w64(kept != 0u);
+        const u32 last = 63u - (u32)__builtin_clzll(has);
+        vstore4(rso, lane == last ? st.out_pos + ttot - 4u : kOOB, T, st.wt);
+        ++rounds;
+    }
     st.out_pos += ttot;
     st.flushed = st.out_pos;
     st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
@@ -1073,8 +1104,9 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
     const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
-    if (kFast && RLE_DEC_FAST && !pr.tail && !st.head) {
-        const u32 r = dec_tile_fast(pr, lane, clut, stage, rso, U, st, kc);
+    if (kFast && RLE_DEC_FAST && !st.head) {
+        const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
+                              : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
         if (r != kNotFast) return r;
     }
     const DecLen ln = dec_lengths(pr, st.d);

@@ -1,0 +1,126 @@
+"""GPU parity of the decode's literal-tile fast path (csrc/rle_device.h dec_tile_fast) against
+the oracle: crafted streams of literals and "vv2" pairs, the tiles the fast path takes, mixed with
+pairs of other counts and run-heavy stretches (tiles the general path takes), with pairs placed
+across tile edges, ragged tails, and decoded sizes that are exact, too large (SHORT: zero fill) or
+too small (OVERFLOW: the serial path).  Bit-exact, slots poisoned."""
+import numpy as np
+import pytest
+
+import rle_oracle as O
+from test_gpu_parity import gpu_decode
+
+pytestmark = pytest.mark.gpu
+STEP = 1008   # decode tile step (csrc/rle_device.h kTileStep)
+
+
+def _stream(rng, n_bytes, p_pair, p_other, p_run, forced=()):
+    """Token stream of about n_bytes: literals, pairs "vv2", pairs with another count digit
+    (p_other), and short run-heavy stretches (p_run).  Each token's byte differs from the byte
+    before it, so the decoder's parse is exactly these tokens.  forced: positions where a "vv2"
+    pair must start (when the stream reaches them at a token boundary, else the next one).
+    Returns (stream, decoded length)."""
+    out = bytearray()
+    U = 0
+    forced = sorted(forced)
+    fi = 0
+    prev = -1
+    while len(out) < n_bytes:
+        v = int(rng.integers(0, 256))
+        while v == prev:
+            v = int(rng.integers(0, 256))
+        want_pair = fi < len(forced) and len(out) >= forced[fi]
+        if want_pair:
+            fi += 1
+        r = rng.random()
+        if want_pair or r < p_pair:
+            out += bytes([v, v, ord("2")])
+            U += 2
+            prev = ord("2")
+        elif r < p_pair + p_other:
+            c = int(rng.integers(3, 10))
+            out += bytes([v, v, ord("0") + c])
+            U += c
+            prev = ord("0") + c
+        elif r < p_pair + p_other + p_run:
+            for _ in range(int(rng.integers(2, 12))):
+                c = int(rng.integers(2, 10))
+                out += bytes([v, v, ord("0") + c])
+                U += c
+                prev = ord("0") + c
+                v = (v + 1 + int(rng.integers(0, 254))) % 256
+                while v == prev:
+                    v = (v + 1) % 256
+        else:
+            out += bytes([v])
+            U += 1
+            prev = v
+    return bytes(out), U
+
+
+def _cases():
+    rng = np.random.default_rng(2024)
+    cases = []
+    lengths = [STEP * k + d for k in range(1, 7) for d in (-20, -3, -2, -1, 0, 1, 2, 3, 17)]
+    lengths += [int(x) for x in rng.integers(1, 7000, size=120)]
+    for i, n in enumerate(lengths):
+        p_pair = (0.0, 0.02, 0.1, 0.2, 0.35)[i % 5]
+        p_other = (0.0, 0.0, 0.0005, 0.01)[i % 4]
+        p_run = (0.0, 0.0, 0.0, 0.002)[(i // 4) % 4]
+        cases.append(_stream(rng, n, p_pair, p_other, p_run))
+    # pairs starting at the last owned positions of a tile and just before them
+    for k in (1, 2, 3):
+        for back in (1, 2, 3, 4):
+            cases.append(_stream(rng, STEP * k + 500, 0.02, 0.0, 0.0, forced=(STEP * k - back,)))
+            cases.append(_stream(rng, STEP * (k + 1) + 40, 0.0, 0.0, 0.0, forced=(STEP * k - back, STEP * k + 1)))
+    # a general first tile (count 5) handing a partial chunk to literal tiles, and back
+    for j in range(20):
+        cases.append(_stream(rng, 4000 + 37 * j, 0.05, 0.0, 0.0, forced=()))
+        s, U = cases[-1]
+        cases[-1] = (bytes([65, 65, ord("5")]) + s[1:] if s[0] != 65 else s, None)
+    return cases
+
+
+def _natural_size(s):
+    """Decoded length of a stream whose tokens are all bounded (the generator's streams)."""
+    U, j = 0, 0
+    while j < len(s):
+        if j + 1 < len(s) and s[j] == s[j + 1]:
+            U += s[j + 2] - ord("0") if j + 2 < len(s) else 0
+            j += 3
+        else:
+            U += 1
+            j += 1
+    return U
+
+
+def test_literal_tiles_match_oracle():
+    cases = _cases()
+    streams = [s for s, _ in cases]
+    sizes = [_natural_size(s) for s in streams]
+    for delta in (0, 7, -5):   # exact, SHORT (zero fill), OVERFLOW (serial path)
+        us = [max(0, u + delta) for u in sizes]
+        dec, st = gpu_decode(streams, us)
+        for i, s in enumerate(streams):
+            ref, rst = O.decode(s, us[i])
+            assert dec[i] == ref, (delta, i, len(s), us[i])
+        if delta == 0:
+            assert ((st & 0xFF) == 0).all()
+
+
+def test_literal_tiles_encoder_output_batch():
+    """Encoder output of text-like data (doubled letters are "vv2" pairs): the bench's random kind
+    and literal-heavy tiles with a few pairs per lane, decoded in one batch."""
+    rng = np.random.default_rng(7)
+    xs = []
+    for i in range(400):
+        n = int(rng.integers(1, 20000))
+        alpha = np.frombuffer(b"etaoinshrdlucmfwypvbgkqjxz ", np.uint8)
+        x = rng.choice(alpha, size=n)
+        dup = rng.random(n) < (0.02, 0.05, 0.1)[i % 3]
+        x = np.repeat(x, np.where(dup, 2, 1))[:n]
+        xs.append(x.tobytes())
+    ys = [O.encode(x) for x in xs]
+    dec, st = gpu_decode(ys, [len(x) for x in xs])
+    bad = [i for i in range(len(xs)) if dec[i] != xs[i]]
+    assert not bad, (len(bad), bad[:5])
+    assert ((st & 0xFF) == 0).all()
