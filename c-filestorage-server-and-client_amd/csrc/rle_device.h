@@ -34,6 +34,7 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 constexpr u32 kWave = 64;
 constexpr u32 kMaxBufferBytes = RLE_MAX_BUFFER_BYTES;   // per-buffer limit (32-bit in-buffer offsets)
 constexpr u32 kOOB = 0x80000000u;               // store offset dropped by the range check
+constexpr u32 kNotFast = 0xFFFFFFFEu;           // a fast tile path declined (the general path runs)
 
 // ---------------------------------------------------------------- cross-lane primitives (DPP)
 enum : int {
@@ -174,7 +175,10 @@ __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v, bool wt) {
     case N:                                                   \
         asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
         break;
+// (n is wave-uniform; readfirstlane tells the compiler, which otherwise may lower the switch as an
+// exec-masked VGPR compare tree)
 __device__ __forceinline__ void vm_wait(u32 n) {
+    n = uniform(n);
     switch (n < 15u ? n : 15u) {
         RLE_VMW(0) RLE_VMW(1) RLE_VMW(2) RLE_VMW(3) RLE_VMW(4) RLE_VMW(5) RLE_VMW(6) RLE_VMW(7) RLE_VMW(8)
         RLE_VMW(9) RLE_VMW(10) RLE_VMW(11) RLE_VMW(12) RLE_VMW(13) RLE_VMW(14) RLE_VMW(15)
@@ -502,15 +506,142 @@ __device__ __forceinline__ void enc_pass1(const u32* w, u32 T, u32 P, u32 NS, u3
     }
 }
 
+// ---------------------------------------------------------------- literal tiles (the fast path)
+// A tile with no run longer than 2 (random and text-like data) encodes to its own bytes with a '2'
+// inserted after each pair's second byte.  Each token belongs to the lane of its start, so a lane
+// outputs its 16 bytes, less position 0 when that is the second byte of a pair started before the
+// lane, plus the next lane's byte 0 when a pair starts at position 15, with <= 2 insertions (one
+// LUT-selected v_perm per output dword): n = 15..19 bytes.  One 16-byte store writes its first 16
+// output bytes (with 15, the 16th is the next lane's first: the bytes two lanes store twice are
+// equal), a second one, for n > 16, its last 16.  Not for the last tile: the last owner's store
+// may reach one byte past the tile's output, which the next tile rewrites (that byte is the next
+// tile's first output: a lane outputs 15 bytes only when its position 15 starts a token that
+// does not continue, so the next tile starts a token).  No staging, no pass 2.
+#ifndef RLE_ENC_FAST
+#define RLE_ENC_FAST 1
+#endif
+// Insertion selectors: entry i (the output index of an inserted '2', 0 = none), dword q: the
+// v_perm selector taking output bytes 4q..4q+3 from (S[q] : S[q-1] with bytes 0, 1 = '2').  Two
+// insertions are two passes.  6 dwords per entry (5 used): 8-byte aligned reads.  Each wave
+// LDS-DMAs its own copy (kInsDmaLanes x 16 bytes) ahead of its first tile.
+constexpr u32 kInsEntries = 19u;
+constexpr u32 kInsStride = 6u;
+constexpr u32 kInsWords = kInsEntries * kInsStride;            // 114
+constexpr u32 kInsDmaLanes = (4u * kInsWords + 15u) / 16u;      // 29
+constexpr u32 kInsWaveWords = 4u * kInsDmaLanes;                // 116: one wave's copy
+struct EncInsLut {
+    u32 s[kInsWaveWords];
+};
+constexpr EncInsLut make_ins_lut() {
+    EncInsLut t{};
+    for (u32 i = 0; i < kInsEntries; ++i)
+        for (u32 q = 0; q < 5u; ++q) {
+            u32 sel = 0;
+            for (u32 b = 0; b < 4u; ++b) {
+                const u32 m = 4u * q + b;
+                u32 v = 0;
+                if (!(i && m == i)) v = m - ((i && i < m) ? 1u : 0u) - 4u * q + 4u;   // 3..7
+                sel |= v << (8u * b);
+            }
+            t.s[i * kInsStride + q] = sel;
+        }
+    return t;
+}
+static __constant__ EncInsLut kEncInsLut = make_ins_lut();
+
+// Returns the store instructions issued, or kNotFast (nothing done: the general path encodes the
+// tile).  Only for tiles before the last one, with st.head == 0.
 template <bool k64>
+__device__ __forceinline__ u32 enc_tile_fast(const EncAn& a, const uint2 look, u32 pos, u32 lane, const u32* elut,
+                                             uint8_t* stage, u32x4 rso, EncState& st) {
+    constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;
+    constexpr uint64_t kOwnedMask = k64 ? ~0ull : (1ull << kOwnLanes) - 1ull;
+    const bool owned = k64 || lane < kOwnLanes;
+    // continuations (bit j: byte j equals byte j-1) of the lane's 16 positions and the next lane's
+    // first two; pairs: run starts whose run continues
+    // (runs of 3+ first, in as few instructions as possible: run-heavy tiles leave here)
+    const u32 C18 = ~a.B24 & 0x3FFFFu;
+    if (__builtin_amdgcn_ballot_w64(((C18 & (C18 >> 1)) != 0u) && owned)) return kNotFast;
+    const u32 P = a.B & ~(a.B24 >> 1) & 0xFFFFu;
+    if (__builtin_amdgcn_ballot_w64(__builtin_popcount(P) > 2 && owned)) return kNotFast;
+    if ((readlane(C18, 0) & 1u) && st.rs + 1u != pos) return kNotFast;   // the run entering is longer
+    const u32 del0 = C18 & 1u;
+    const u32 nout = owned ? 16u - del0 + ((P >> 15) & 1u) + (u32)__builtin_popcount(P) : 0u;
+    const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
+    const u32 ttot = readlane(oincl, 63);
+
+    u32 rounds = 0;
+    const u32 rel0 = st.out_pos - st.flushed;
+    if (rel0) {   // a general tile's partial chunk (its bytes past rel0 are rewritten below)
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16u);
+        vstore(rso, lane == 0u ? st.flushed : kOOB, v, st.wt);
+        rounds = 1;
+    }
+    // source bytes S' (the lane's 16 and the next lane's first, less position 0 when deleted)
+    const u32* w = a.w;
+    const u32 nw0 = from_next_lane(w[0], 0u);   // (all lanes: a DPP inside the select may run with lane 63 off)
+    const u32 s4 = (k64 && lane == 63u) ? look.x : nw0;
+    const u32 sh = 8u * del0;
+    const u32 Sp[5] = {alignbyte(w[1], w[0], del0), alignbyte(w[2], w[1], del0), alignbyte(w[3], w[2], del0),
+                       alignbyte(s4, w[3], del0), s4 >> sh};
+    const u32 j1 = (u32)__builtin_ctz(P | 0x10000u), j2 = (u32)__builtin_ctz((P & (P - 1u)) | 0x10000u);
+    const u32 k2 = 0x32323232u;
+    typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+    // one insertion pass: out[q] = bytes of in[] with a '2' at output index i (0: none)
+    auto insert = [&](const u32* in, u32 i, u32* out) {
+        const u32* e = elut + i * kInsStride;
+        const u32x2 e01 = *reinterpret_cast<const u32x2*>(e), e23 = *reinterpret_cast<const u32x2*>(e + 2),
+                    e45 = *reinterpret_cast<const u32x2*>(e + 4);
+        out[0] = __builtin_amdgcn_perm(in[0], k2, e01.x);
+        out[1] = __builtin_amdgcn_perm(in[1], __builtin_amdgcn_perm(in[0], k2, 0x07060100u), e01.y);
+        out[2] = __builtin_amdgcn_perm(in[2], __builtin_amdgcn_perm(in[1], k2, 0x07060100u), e23.x);
+        out[3] = __builtin_amdgcn_perm(in[3], __builtin_amdgcn_perm(in[2], k2, 0x07060100u), e23.y);
+        out[4] = __builtin_amdgcn_perm(in[4], __builtin_amdgcn_perm(in[3], k2, 0x07060100u), e45.x);
+    };
+    u32 out[5];
+    insert(Sp, j1 < 16u ? j1 + 2u - del0 : 0u, out);
+    if (__builtin_amdgcn_ballot_w64(j2 < 16u)) {   // second pairs (the '2' after the first counts)
+        const u32 o1[5] = {out[0], out[1], out[2], out[3], out[4]};
+        insert(o1, j2 < 16u ? j2 + 3u - del0 : 0u, out);
+    }
+    // the first 16 output bytes (with 15, the next lane's first byte last)
+    const u32 n0 = from_next_lane(out[0], 0u);
+    u32x4 va;
+    va.x = out[0]; va.y = out[1]; va.z = out[2];
+    va.w = __builtin_amdgcn_perm(n0, out[3], nout >= 16u ? 0x03020100u : 0x04020100u);
+    const u32 o = st.out_pos + oincl - nout;
+    vstore(rso, owned ? o : kOOB, va, st.wt);
+    // the last 16, where there are more than 16
+    if (__builtin_amdgcn_ballot_w64(nout > 16u)) {
+        const u32 b = nout - 16u;
+        u32x4 vb;
+        vb.x = alignbyte(out[1], out[0], b); vb.y = alignbyte(out[2], out[1], b);
+        vb.z = alignbyte(out[3], out[2], b); vb.w = alignbyte(out[4], out[3], b);
+        vstore(rso, nout > 16u ? o + b : kOOB, vb, st.wt);
+        ++rounds;
+    }
+    st.out_pos += ttot;
+    st.flushed = st.out_pos;
+    st.prev_top = readlane(a.top, kLast);
+    const u32 i63 = readlane(a.incl, kLast);
+    st.rs = i63 > st.rs ? i63 : st.rs;
+    return rounds + 1u;
+}
+
+template <bool k64, bool kFast = false>
 __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
                                         u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
-                                        const EncK& kc) {
+                                        const EncK& kc, const u32* elut = nullptr) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     const uint2 look = k64 ? *reinterpret_cast<const uint2*>(cslot + kSlot) : uint2{0u, 0u};
     next();   // the slot is free once read
-    const EncAn an = enc_analyze<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, st.rs, kc);
+    EncAn an = enc_analyze_bounds<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, kc);
+    if (kFast && RLE_ENC_FAST && !st.head && pos + (k64 ? kEncStep : kTileStep) < Uo) {
+        const u32 r = enc_tile_fast<k64>(an, look, pos, lane, elut, stage, rso, st);
+        if (r != kNotFast) return r;
+    }
+    enc_tokens(an, st.rs);
     constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;   // the tile's last owning lane
     const u32* w = an.w;
     const u32 validm = an.validm, top = an.top, B24 = an.B24, incl = an.incl, T = an.T, P = an.P;
@@ -967,7 +1098,6 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
 #ifndef RLE_DEC_FAST
 #define RLE_DEC_FAST 1
 #endif
-constexpr u32 kNotFast = 0xFFFFFFFEu;
 // Compaction selectors: entry 17 t1 + t2 (a lane's deleted positions t1 < t2, 16 = none), dword q:
 // the v_perm selector taking output bytes 4q..4q+3 from (y[q+1]:y[q]) once t1, t2 are removed.
 constexpr u32 kCompactEntries = 17u * 17u;

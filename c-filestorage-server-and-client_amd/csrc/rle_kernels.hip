@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     const unsigned long long tl0 = tl_now();
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * 2 * kEncSlot];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kEncWaves * kEncStage];
+    __shared__ __attribute__((aligned(16))) u32 elut_all[kEncWaves * kInsWaveWords];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     uint8_t* stage = stage_all + wid * kEncStage;
@@ -111,6 +112,12 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
         }
         return;
     }
+    // this wave's copy of the insertion selectors (enc_tile_fast), by LDS-DMA ahead of the first
+    // tile's: loads complete in issue order, so walk_tiles' wait for tile 0 covers it (no tile, no
+    // load: nothing may land in LDS after the wave ends)
+    const u32* elut = elut_all + wid * kInsWaveWords;
+    if (U64 != 0u && !RLE_NOWALK && lane < kInsDmaLanes)
+        dma_tile(make_rsrc(&kEncInsLut, 4u * kInsWaveWords), 16u * lane, uniform(lds_addr(elut)));
     const u32 U = (u32)U64;
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
@@ -127,12 +134,12 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
         walk_tiles<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
                                    [&](u32 t, const uint8_t* cs, const Refill& nx) {
                                        tl_mark(b, 2u + t, lane);
-                                       return enc_tile<true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc);
+                                       return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
                                    });
     else
         walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
             tl_mark(b, 2u + t, lane);
-            return enc_tile<false>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc);
+            return enc_tile<false, true>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc, elut);
         });
     RLE_STAMP(st.sp, 6);   // drain
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C

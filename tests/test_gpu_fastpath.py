@@ -124,3 +124,39 @@ def test_literal_tiles_encoder_output_batch():
     bad = [i for i in range(len(xs)) if dec[i] != xs[i]]
     assert not bad, (len(bad), bad[:5])
     assert ((st & 0xFF) == 0).all()
+
+
+def _pairs_data(rng, n, p_dup, p_triple=0.0, forced=()):
+    """Bytes with no equal neighbours except doubled bytes (p_dup per byte), the odd triple
+    (p_triple: a tile the encoder's fast path declines), and doubles at the forced positions."""
+    x = rng.integers(0, 255, size=n, dtype=np.int64)
+    x = np.where(x >= np.roll(x, 1), x + 1, x)      # break most accidental repeats
+    x[1:] = np.where(x[1:] == x[:-1], (x[1:] + 1) % 256, x[1:])
+    x = x.astype(np.uint8)
+    dup = rng.random(n) < p_dup
+    tri = rng.random(n) < p_triple
+    y = np.repeat(x, np.where(tri, 3, np.where(dup, 2, 1)))[:n].copy()
+    for f in forced:   # a pair starting exactly at f, then a different byte
+        if 0 < f and f + 2 < n:
+            y[f] = y[f - 1] ^ 0x55
+            y[f + 1] = y[f]
+            y[f + 2] = y[f] ^ 0x0F
+    return y.tobytes()
+
+
+def test_literal_tiles_encode_match_oracle():
+    """Encoder fast path (csrc/rle_device.h enc_tile_fast): literal and pair tiles, pairs at the
+    edges of 1024-byte tiles (buffers <= 16 KiB) and 1008-byte tiles (larger), runs of 3 that
+    make a tile decline, ragged sizes; output bit-exact and nothing written past C."""
+    from test_gpu_parity import _oracle_parity
+    rng = np.random.default_rng(11)
+    xs = []
+    for i in range(300):
+        n = int(rng.integers(1, 40000))
+        xs.append(_pairs_data(rng, n, (0.0, 0.01, 0.05, 0.12, 0.3)[i % 5], (0.0, 0.0, 0.0002, 0.003)[i % 4]))
+    for k in range(1, 8):
+        for d in (-3, -2, -1, 0, 1):
+            xs.append(_pairs_data(rng, 1024 * k + 300, 0.01, forced=(1024 * k + d,)))
+            xs.append(_pairs_data(rng, 17000 + 1008 * k, 0.01, forced=(1008 * k + d, 1008 * k + d + 5)))
+            xs.append(_pairs_data(rng, 1024 * k + d + 2, 0.02))
+    _oracle_parity(xs)
