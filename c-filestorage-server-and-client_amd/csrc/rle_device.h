@@ -555,8 +555,7 @@ template <bool k64>
 __device__ __forceinline__ u32 enc_tile_fast(const EncAn& a, const uint2 look, u32 pos, u32 lane, const u32* elut,
                                              uint8_t* stage, u32x4 rso, EncState& st) {
     constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;
-    constexpr uint64_t kOwnedMask = k64 ? ~0ull : (1ull << kOwnLanes) - 1ull;
-    const bool owned = k64 || lane < kOwnLanes;
+        const bool owned = k64 || lane < kOwnLanes;
     // continuations (bit j: byte j equals byte j-1) of the lane's 16 positions and the next lane's
     // first two; pairs: run starts whose run continues
     // (runs of 3+ first, in as few instructions as possible: run-heavy tiles leave here)
@@ -628,6 +627,86 @@ __device__ __forceinline__ u32 enc_tile_fast(const EncAn& a, const uint2 look, u
     return rounds + 1u;
 }
 
+// A tile that is one run (no run boundary past its first byte: zero data, long runs) encodes to
+// the tokens "v v '9'" every 9 bytes from the run start, the last one's count from the bytes after
+// the tile (up to 8 lookahead boundary bits), or a lone "v" when that count is 1.  Its output is
+// then a 3-periodic pattern: lane c forms staged chunk c (the partial chunk's bytes first) and
+// the flush stores it; the new partial chunk goes back to the staging.  Not for the last tile.
+__device__ __forceinline__ u32 rep_byte(u32 v) { return __builtin_amdgcn_perm(0u, v, 0u); }
+template <bool k64>
+__device__ __forceinline__ u32 enc_tile_run(const EncAn& a, u32 pos, u32 lane, uint8_t* stage, u32x4 rso,
+                                            EncState& st) {
+    constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;
+    constexpr u32 kStep = k64 ? kEncStep : kTileStep;
+    const bool owned = k64 || lane < kOwnLanes;
+    if (__builtin_amdgcn_ballot_w64((a.B & (lane == 0u ? 0xFFFEu : 0xFFFFu)) != 0u && owned)) return kNotFast;
+    const u32 rs = (readlane(a.B, 0) & 1u) ? pos : st.rs;     // the run's start
+    const u32 f = pos + (9u - (pos - rs) % 9u) % 9u;          // first token start in the tile
+    const u32 ns = (pos + kStep - f + 8u) / 9u;               // token starts in the tile (>= 1)
+    const u32 sl = f + 9u * (ns - 1u);
+    const u32 ext = (u32)__builtin_ctz((readlane(a.B24, kLast) >> 16) | 0x100u);   // run bytes past the tile
+    const u32 cl = pos + kStep + ext - sl < 9u ? pos + kStep + ext - sl : 9u;     // last token's count
+    const u32 tot = 3u * (ns - 1u) + (cl >= 2u ? 3u : 1u);
+    const u32 v = readlane(a.w[0], 0) & 0xFFu;
+    const u32 rel0 = st.out_pos - st.flushed;
+    const u32 rel = rel0 + tot, nfl = rel >> 4;
+    // lane c: staged chunk c = output bytes k = 16 c + i - rel0 of this tile (k < 0: the old partial)
+    const u32 k0 = 16u * lane - rel0;                         // may wrap for lane 0
+    const u32 ph = (16u * lane + 48u - rel0) % 3u;            // k0 mod 3
+    const u32 vv = rep_byte(v), d9 = 0x39393939u;
+    // byte i is the count digit where (ph + i) % 3 == 2
+    u32 o[4];
+#pragma unroll
+    for (u32 q = 0; q < 4u; ++q) {
+        // digit masks for phase 0, 1, 2 of dword q (i = 4q + b, digit when (ph + i) % 3 == 2)
+        u32 mk[3];
+#pragma unroll
+        for (u32 p = 0; p < 3u; ++p) {
+            u32 m = 0;
+            for (u32 b = 0; b < 4u; ++b)
+                if ((p + 4u * q + b) % 3u == 2u) m |= 0xFFu << (8u * b);
+            mk[p] = m;
+        }
+        const u32 dm = ph == 0u ? mk[0] : ph == 1u ? mk[1] : mk[2];
+        o[q] = (vv & ~dm) | (d9 & dm);
+    }
+    // the last token: count cl (digit at k = tot - 1 when cl >= 2)
+    if (cl != 9u && cl >= 2u) {
+        const u32 kd = tot - 1u - k0;                          // byte index in this lane's chunk
+        if (kd < 16u) {
+            const u32 sh = 8u * (kd & 3u);
+            const u32 dv = (0x30u + cl) << sh, msk = 0xFFu << sh;
+            const u32 q = kd >> 2;
+            o[0] = q == 0u ? (o[0] & ~msk) | dv : o[0];
+            o[1] = q == 1u ? (o[1] & ~msk) | dv : o[1];
+            o[2] = q == 2u ? (o[2] & ~msk) | dv : o[2];
+            o[3] = q == 3u ? (o[3] & ~msk) | dv : o[3];
+        }
+    }
+    // chunk 0: the old partial chunk's rel0 bytes first
+    const u32x4 old = *reinterpret_cast<const u32x4*>(stage + 16u);
+    if (lane == 0u && rel0) {
+        const u32 ov[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+        for (u32 q = 0; q < 4u; ++q) {
+            const u32 nb = rel0 > 4u * q ? (rel0 - 4u * q < 4u ? rel0 - 4u * q : 4u) : 0u;
+            const u32 m = lowmask(8u * nb);
+            o[q] = (ov[q] & m) | (o[q] & ~m);
+        }
+    }
+    const u32x4 ov4 = u32x4{o[0], o[1], o[2], o[3]};
+    vstore(rso, lane < nfl ? st.flushed + 16u * lane : kOOB, ov4, st.wt);
+    wave_lds_sync();   // every lane has read the old partial chunk
+    if (lane == nfl) *reinterpret_cast<u32x4*>(stage + 16u) = ov4;   // the new partial chunk
+    wave_lds_sync();
+    st.flushed += 16u * nfl;
+    st.out_pos += tot;
+    st.prev_top = readlane(a.top, kLast);
+    const u32 i63 = readlane(a.incl, kLast);
+    st.rs = i63 > st.rs ? i63 : st.rs;
+    return 1u;
+}
+
 template <bool k64, bool kFast = false>
 __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
                                         u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
@@ -638,7 +717,9 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     next();   // the slot is free once read
     EncAn an = enc_analyze_bounds<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, kc);
     if (kFast && RLE_ENC_FAST && !st.head && pos + (k64 ? kEncStep : kTileStep) < Uo) {
-        const u32 r = enc_tile_fast<k64>(an, look, pos, lane, elut, stage, rso, st);
+        u32 r = enc_tile_run<k64>(an, pos, lane, stage, rso, st);
+        if (r != kNotFast) return r;
+        r = enc_tile_fast<k64>(an, look, pos, lane, elut, stage, rso, st);
         if (r != kNotFast) return r;
     }
     enc_tokens(an, st.rs);

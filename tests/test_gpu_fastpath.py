@@ -160,3 +160,34 @@ def test_literal_tiles_encode_match_oracle():
             xs.append(_pairs_data(rng, 17000 + 1008 * k, 0.01, forced=(1008 * k + d, 1008 * k + d + 5)))
             xs.append(_pairs_data(rng, 1024 * k + d + 2, 0.02))
     _oracle_parity(xs)
+
+
+def test_run_tiles_encode_match_oracle():
+    """Encoder run tiles (csrc/rle_device.h enc_tile_run): runs spanning whole tiles, starting at
+    every phase mod 9 before a tile edge and ending 0..10 bytes past one (the last token's count
+    from the lookahead bits, a lone byte for count 1), runs of 0x00 and of digits, literal and pair
+    tiles after them (the staged partial chunk handed over), both tile forms (<= 16 KiB: 1024-byte
+    tiles, larger: 1008)."""
+    from test_gpu_parity import _oracle_parity
+    rng = np.random.default_rng(5)
+    xs = []
+    for step, base in ((1024, 0), (1008, 17000)):
+        for k in (1, 2, 3):
+            edge = base + step * k
+            for start_back in (0, 1, 4, 8, 9, 17, 700):
+                for end_past in (0, 1, 2, 7, 8, 9, 10):
+                    n = edge + 2500
+                    x = bytearray(_pairs_data(rng, n, 0.03))
+                    s0 = max(0, edge - step - start_back)
+                    e0 = min(n, edge + end_past)
+                    v = (0x00, ord("9"), 0x41)[(k + end_past) % 3]
+                    x[s0:e0] = bytes([v]) * (e0 - s0)
+                    if e0 < n and x[e0] == v:
+                        x[e0] = v ^ 1
+                    xs.append(bytes(x))
+    for i in range(60):   # long runs of random lengths, random values, ragged sizes
+        n = int(rng.integers(1, 60000))
+        lens = rng.integers(1, 5000, size=64)
+        vals = rng.integers(0, 4, size=64)
+        xs.append(np.repeat(vals.astype(np.uint8), lens)[:n].tobytes())
+    _oracle_parity(xs)
