@@ -1179,26 +1179,25 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
 #ifndef RLE_DEC_FAST
 #define RLE_DEC_FAST 1
 #endif
-// Compaction selectors: entry 17 t1 + t2 (a lane's deleted positions t1 < t2, 16 = none), dword q:
-// the v_perm selector taking output bytes 4q..4q+3 from (y[q+1]:y[q]) once t1, t2 are removed.
-constexpr u32 kCompactEntries = 17u * 17u;
+// Compaction selectors: entry t (a deleted position, 16 = none), dword q: the v_perm selector
+// taking output bytes 4q..4q+3 from (y[q+1]:y[q]) once position t is removed.  A lane's two
+// deletions are two passes, the higher position first.  17 entries of 16 bytes: every wave
+// LDS-DMAs them (with the phase table) into the workgroup's copy ahead of its first tile.
+constexpr u32 kCompactEntries = 17u;
 struct DecCompactLut {
     u32 s[kCompactEntries * 4u];
 };
 constexpr DecCompactLut make_compact_lut() {
     DecCompactLut t{};
-    for (u32 t1 = 0; t1 <= 16u; ++t1)
-        for (u32 t2 = 0; t2 <= 16u; ++t2)
-            for (u32 q = 0; q < 4u; ++q) {
-                u32 sel = 0;
-                for (u32 b = 0; b < 4u; ++b) {
-                    const u32 m = 4u * q + b;
-                    const u32 s = m + ((t1 < 16u && m >= t1) ? 1u : 0u) + ((t2 < 16u && t2 > t1 && m + 1u >= t2) ? 1u : 0u);
-                    const u32 v = s - 4u * q;
-                    sel |= (v > 7u ? 7u : v) << (8u * b);
-                }
-                t.s[(17u * t1 + t2) * 4u + q] = sel;
+    for (u32 d = 0; d <= 16u; ++d)
+        for (u32 q = 0; q < 4u; ++q) {
+            u32 sel = 0;
+            for (u32 b = 0; b < 4u; ++b) {
+                const u32 m = 4u * q + b;
+                sel |= (m + (m >= d ? 1u : 0u) - 4u * q) << (8u * b);   // 0..4
             }
+            t.s[d * 4u + q] = sel;
+        }
     return t;
 }
 static __constant__ DecCompactLut kCompactLut = make_compact_lut();
@@ -1274,12 +1273,22 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     const u32 dm = lane < kOwnLanes ? del : 0u;
     const u32 t1 = (u32)__builtin_ctz(dm | 0x10000u);
     const u32 t2 = (u32)__builtin_ctz((dm & (dm - 1u)) | 0x10000u);
-    const u32x4 sel = clut[17u * t1 + t2];
+    // remove t2 (if any lane has a second deletion), then t1
+    u32 y[4] = {w[0], w[1], w[2], w[3]};
+    if (__builtin_amdgcn_ballot_w64(t2 < 16u)) {
+        const u32x4 s2 = clut[t2];
+        const u32 y3 = __builtin_amdgcn_perm(y[3], y[3], s2.w);
+        y[0] = __builtin_amdgcn_perm(y[1], y[0], s2.x);
+        y[1] = __builtin_amdgcn_perm(y[2], y[1], s2.y);
+        y[2] = __builtin_amdgcn_perm(y[3], y[2], s2.z);
+        y[3] = y3;
+    }
+    const u32x4 sel = clut[t1];
     u32x4 o;
-    o.x = __builtin_amdgcn_perm(w[1], w[0], sel.x);
-    o.y = __builtin_amdgcn_perm(w[2], w[1], sel.y);
-    o.z = __builtin_amdgcn_perm(w[3], w[2], sel.z);
-    const u32 c3 = __builtin_amdgcn_perm(w[3], w[3], sel.w);
+    o.x = __builtin_amdgcn_perm(y[1], y[0], sel.x);
+    o.y = __builtin_amdgcn_perm(y[2], y[1], sel.y);
+    o.z = __builtin_amdgcn_perm(y[3], y[2], sel.z);
+    const u32 c3 = __builtin_amdgcn_perm(y[3], y[3], sel.w);
     // bytes kept..15 of the store: the next lane's first bytes (kept >= 14 on full owned lanes;
     // fewer only where the output ends)
     const u32 n0 = from_next_lane(o.x, 0u);

@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const unsigned long long tl0 = tl_now();
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kDecStage];
-    __shared__ DecEntry tbl[256];
+    __shared__ __attribute__((aligned(16))) DecEntry tbl[256];
     __shared__ u32x4 clut[kCompactEntries];
 #ifdef RLE_LDS_PAD   // occupancy experiments only
     __shared__ uint8_t ldspad[RLE_LDS_PAD];
@@ -285,22 +285,6 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
 #endif
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
-    // Setup order overlaps latencies: the buffer's metadata and the phase table are loaded
-    // together, and the first two tiles' DMA is issued before the staging is zeroed.  (The table
-    // is stored first: the compiler does not count the DMA loads, so a wait for the table after
-    // them would wait for them too.)
-    constexpr u32 kTblPer = (256u + kDecBlock - 1u) / kDecBlock;
-    DecEntry te[kTblPer];
-#pragma unroll
-    for (u32 i = 0; i < kTblPer; ++i) te[i] = dec_entry_from(kDecTable.e[(threadIdx.x + i * kDecBlock) & 255u]);
-    constexpr u32 kLutPer = (kCompactEntries + kDecBlock - 1u) / kDecBlock;
-    u32x4 ce[kLutPer];
-#pragma unroll
-    for (u32 i = 0; i < kLutPer; ++i) {
-        const u32 e = threadIdx.x + i * kDecBlock;
-        const u32* s = &kCompactLut.s[4u * (e < kCompactEntries ? e : 0u)];
-        ce[i] = u32x4{s[0], s[1], s[2], s[3]};
-    }
     // with an issue order, workgroups take its ranks in dispatch order (the heavy buffers first,
     // spread over every XCD); else each XCD takes a contiguous slice of the batch
     u32 b;
@@ -326,17 +310,24 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const u32 ntiles = (b < n && !bad && !RLE_NOWALK) ? ntiles_for(C) : 0u;
     uint8_t* stage = stage_all + wid * kDecStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-#pragma unroll
-    for (u32 i = 0; i < kTblPer; ++i) tbl[(threadIdx.x + i * kDecBlock) & 255u] = te[i];
-#pragma unroll
-    for (u32 i = 0; i < kLutPer; ++i)
-        if (threadIdx.x + i * kDecBlock < kCompactEntries) clut[threadIdx.x + i * kDecBlock] = ce[i];
+    // The phase table and the compaction selectors: every wave with tiles to walk LDS-DMAs both
+    // into the workgroup's copy (the same bytes, so the waves' writes agree) ahead of its first
+    // tile's load.  Loads complete in issue order, so walk_tiles' wait for tile 0 covers them and no
+    // barrier is needed; a wave without tiles issues none (nothing may land after it ends).
+    if (ntiles) {
+        const u32x4 rt = make_rsrc(&kDecTable, (u32)sizeof(DecTable));
+        const u32 lt = uniform(lds_addr(tbl));
+        asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
+        dma_tile(rt, 16u * lane, lt);
+        dma_tile(rt, 1024u + 16u * lane, lt + 1024u);
+        if (lane < kCompactEntries)
+            dma_tile(make_rsrc(&kCompactLut, (u32)sizeof(DecCompactLut)), 16u * lane, uniform(lds_addr(clut)));
+    }
     stagger();
     walk_prime(rsi, 0u, ntiles, lane, slots);
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
-    if (kDecWaves > 1) __syncthreads();
-    else wave_lds_sync();
+    wave_lds_sync();
 
     if (b < n) {
         if (bad) {
