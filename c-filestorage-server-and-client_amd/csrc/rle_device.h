@@ -1316,6 +1316,53 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     return rounds + 1u;
 }
 
+// Single-value tile (dec_tile): ttot copies of v after the staged partial chunk.
+__device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st,
+                                             const DecPrep& pr) {
+    const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl = total >> 4;
+    const u32 vv = rep4(v);
+    // chunk 0: the staged positions [0, rel0) filled like a flush, then v (every lane computes it)
+    u32x4 a, b;
+    dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), a, b);
+    u32 L[8];
+    dec_fill_scan(a, b, L);
+    const u32x4 f = dec_fill_out(L, st.fillc);
+    const u32 fv[4] = {f.x, f.y, f.z, f.w};
+    u32 c0[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 nb = rel0 > 4u * k ? (rel0 - 4u * k < 4u ? rel0 - 4u * k : 4u) : 0u;
+        const u32 m = lowmask(8u * nb);
+        c0[k] = (fv[k] & m) | (vv & ~m);
+    }
+    const u32 rounds = (nfl + kWave - 1u) / kWave;
+    for (u32 k = 0; k < rounds; ++k) {
+        const u32 c = k * kWave + lane;
+        const u32x4 o = c == 0u ? u32x4{c0[0], c0[1], c0[2], c0[3]} : u32x4{vv, vv, vv, vv};
+        vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, o, st.wt);
+    }
+    wave_lds_sync();   // every lane has read staging chunk 1
+    // staging chunk 1 = the new partial chunk: the old keys plus a key at rel0 (nothing flushed),
+    // else a key at position 0 (when anything is left) and zeros
+    const u32 kv = kKeyFlag | v;
+    if (lane == 0u) {
+        if (nfl == 0u) {
+            *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(lds_addr(stage) + 32u + 2u * rel0)) = (uint16_t)kv;
+        } else {
+            const u32 k0 = (total & 15u) ? kv : 0u;
+            *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(stage) + 32u)) = u32x4{k0, 0u, 0u, 0u};
+            *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(stage) + 48u)) = u32x4{0u, 0u, 0u, 0u};
+        }
+    }
+    wave_lds_sync();
+    st.fillc = v;
+    st.flushed += 16u * nfl;
+    st.out_pos += ttot;
+    st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
+    st.prev = readlane(pr.w[3], kOwnLanes - 1u);
+    return rounds;
+}
+
 template <bool kFast = false>
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
                                         u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
@@ -1346,6 +1393,21 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
         }
     }
 
+    // A tile whose tokens all carry one byte v and that expands >= 2.86x (zero-filled data: "v v 9"
+    // tokens) decodes to ttot copies of v: the partial chunk staged so far, filled, then rep4(v)
+    // chunks, stored without the scatter and the fill; the new partial chunk is one key.
+    if (kFast && RLE_DEC_FAST && kDecOnePass && !st.head && ttot >= 2880u) {
+        const u32 v = (readlane(w[0], 0) >> (8u * st.d)) & 0xFFu;   // the tile's first token byte
+        const u32 vv = rep4(v);
+        u32 bad = 0;
+#pragma unroll
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 t = w[k] ^ vv;
+            bad |= bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80) & ln.S80[k];
+        }
+        if (!(__builtin_amdgcn_ballot_w64(bad != 0u) & kOwned))
+            return dec_tile_fill(v, ttot, lane, stage, rso, st, pr);
+    }
     RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
     // With the full staging (kDecChunks >= 191) a tile is one pass.  Smaller staging (more waves per
     // SIMD) stages and flushes a tile in passes over consecutive lanes, each as much as fits: a pass
@@ -1401,6 +1463,7 @@ __device__ __forceinline__ void dec_finish(const DecState& st, u32 end, u32 lane
     const u32 rel = st.out_pos - st.flushed;   // < 16
     const u32 span = end - st.flushed;
     const u32 nq = (span + 15u) >> 4;
+    if (nq == 0u) return;   // everything stored (a fast tail tile), nothing staged (rel <= span)
     const u32 tv = rep4(st.tail & 0xFFu);
     // chunk 0: the staged positions [0, rel) filled like a flush (every lane computes it from the
     // same two broadcast reads), the rest the tail byte

@@ -191,3 +191,28 @@ def test_run_tiles_encode_match_oracle():
         vals = rng.integers(0, 4, size=64)
         xs.append(np.repeat(vals.astype(np.uint8), lens)[:n].tobytes())
     _oracle_parity(xs)
+
+
+def test_single_value_tiles_decode_match_oracle():
+    """Decoder single-value tiles (csrc/rle_device.h dec_tile_fill): long runs of one byte (count-9
+    pair tokens, >= 2.86x expansion) entered with every staged partial length, ending at every
+    offset around tile edges, followed by literal tiles, ragged sizes, exact / short / overflow U."""
+    rng = np.random.default_rng(9)
+    xs = []
+    for n in [1008 * k + d for k in range(1, 6) for d in (-40, -9, -1, 0, 1, 9, 333)]:
+        for lead in (0, 1, 5, 15, 16, 17, 31):
+            x = bytearray(_pairs_data(rng, n + lead + 500, 0.02))
+            v = int(rng.integers(0, 256))
+            x[lead:lead + n * 3] = bytes([v]) * min(n * 3, len(x) - lead)
+            xs.append(bytes(x[: lead + n * 3 + 200]))
+    for i in range(40):
+        n = int(rng.integers(1, 200000))
+        lens = rng.integers(1, 30000, size=16)
+        xs.append(np.repeat(rng.integers(0, 256, size=16).astype(np.uint8), lens)[:n].tobytes())
+    ys = [O.encode(x) for x in xs]
+    for delta in (0, 5, -3):
+        us = [max(0, len(x) + delta) for x in xs]
+        dec, st = gpu_decode(ys, us)
+        for i, y in enumerate(ys):
+            ref, _ = O.decode(y, us[i])
+            assert dec[i] == ref, (delta, i, len(xs[i]))
