@@ -1363,7 +1363,8 @@ __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t*
     return rounds;
 }
 
-template <bool kFast = false>
+// kChunks: the staging's chunks per wave (kDecChunks unless a kernel picks its own).
+template <bool kFast = false, u32 kChunks = kDecChunks>
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
                                         u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
                                         DecState& st, const DecK& kc, const u32x4* clut = nullptr) {
@@ -1393,10 +1394,11 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
         }
     }
 
-    // A tile whose tokens all carry one byte v and that expands >= 2.86x (zero-filled data: "v v 9"
-    // tokens) decodes to ttot copies of v: the partial chunk staged so far, filled, then rep4(v)
+    // A tile whose tokens all carry one byte v and that expands >= 20/7 = 2.86x its bytes (zero-
+    // filled data: "v v 9" tokens) decodes to ttot copies of v: the partial chunk staged so far, filled, then rep4(v)
     // chunks, stored without the scatter and the fill; the new partial chunk is one key.
-    if (kFast && RLE_DEC_FAST && kDecOnePass && !st.head && ttot >= 2880u) {
+    if (kFast && RLE_DEC_FAST && !st.head &&
+        7u * ttot >= 20u * (C - pos < kTileStep ? C - pos : kTileStep)) {   // (C > pos: the tile exists)
         const u32 v = (readlane(w[0], 0) >> (8u * st.d)) & 0xFFu;   // the tile's first token byte
         const u32 vv = rep4(v);
         u32 bad = 0;
@@ -1418,10 +1420,13 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     for (;;) {
         const u32 rel0 = st.out_pos + done - st.flushed;
         u32 upto = kOwnLanes, pass = ttot - done;
-        if (!kDecOnePass && rel0 + pass > kDecPassCap) {
+        constexpr bool kOnePass = kChunks >= 191u;
+        constexpr u32 kPassCap = 16u * kChunks - 17u;
+        static_assert(kChunks >= 16u, "a pass must hold at least one lane's output (144 B) past rel < 16");
+        if (!kOnePass && rel0 + pass > kPassCap) {
             // lanes whose output ends within the staging; a prefix, since oincl is monotonic, and it
             // reaches past `from` (a lane decodes at most 144 bytes, rel0 < 16)
-            const uint64_t fit = __builtin_amdgcn_ballot_w64(oincl <= done + kDecPassCap - rel0) & kOwned;
+            const uint64_t fit = __builtin_amdgcn_ballot_w64(oincl <= done + kPassCap - rel0) & kOwned;
             upto = (u32)__builtin_popcountll(fit);
             pass = readlane(oincl, upto - 1u) - done;
         }
@@ -1515,8 +1520,8 @@ __device__ __forceinline__ u32 dec_tiled_status(const DecState& st, u32 U) {
 // streams the tiled path declines: counts outside '1'..'9', unbounded counts before the last
 // token, or streams that decode to more than U bytes.  One lane; the encoder never emits these.
 __device__ u32 dec_serial(const uint8_t* src, u32 C, u32 U, uint64_t cap, uint8_t* dst, u32 lane,
-                          uint8_t* stage) {
-    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
+                          uint8_t* stage, u32 stage_bytes = kDecStage) {
+    for (u32 k = lane; k < stage_bytes / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     for (uint64_t c = lane; c * 16u < cap; c += kWave) {
         if (c * 16u + 16u <= cap) *reinterpret_cast<u32x4*>(dst + c * 16u) = u32x4{0u, 0u, 0u, 0u};

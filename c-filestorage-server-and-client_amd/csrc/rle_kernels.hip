@@ -265,6 +265,11 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
     }
 }
 
+// kChunks: staging chunks per wave (32 B each).  192 hold any tile's output in one pass; the
+// launcher takes 96 (3 KiB per wave: 7 workgroups per CU instead of 4) for batches past one
+// residency round, where the extra waves hide more latency than the two-pass staging of the
+// output-heavy tiles costs.
+template <u32 kChunks>
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
                                                            const uint64_t* __restrict__ in_len,
@@ -276,7 +281,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            const uint32_t* __restrict__ order) {
     const unsigned long long tl0 = tl_now();
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
-    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kDecStage];
+    constexpr u32 kStageB = 32u * kChunks;
+    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kStageB];
     __shared__ __attribute__((aligned(16))) DecEntry tbl[256];
     __shared__ u32x4 clut[kCompactEntries];
 #ifdef RLE_LDS_PAD   // occupancy experiments only
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const u32 C = (u32)C64, U = (u32)U64;
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     const u32 ntiles = (b < n && !bad && !RLE_NOWALK) ? ntiles_for(C) : 0u;
-    uint8_t* stage = stage_all + wid * kDecStage;
+    uint8_t* stage = stage_all + wid * kStageB;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
     // The phase table and the compaction selectors: every wave with tiles to walk LDS-DMAs both
     // into the workgroup's copy (the same bytes, so the waves' writes agree) ahead of its first
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     }
     stagger();
     walk_prime(rsi, 0u, ntiles, lane, slots);
-    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
+    for (u32 k = lane; k < kStageB / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     wave_lds_sync();
 
@@ -346,12 +352,12 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             rsi, 0u, ntiles, lane, slots,
             [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 tl_mark(b, 2u + t, lane);
-                return dec_tile<true>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
+                return dec_tile<true, kChunks>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
             },
             true);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
-        if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage);
+        if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage, kStageB);
         else {
             dec_finish(st, U, lane, stage, rso, dst);
             stat = dec_tiled_status(st, U);
@@ -482,6 +488,10 @@ uint32_t store_policy(uint32_t n, bool enc) {
 // Decode batches past one residency round of the chip (4 workgroups of 4 waves per CU) are
 // issued longest first; RLE_MI355X_DEC_ORDER=0 turns that off.
 constexpr uint32_t kDecRound = 4096;
+#ifndef RLE_DEC_CHUNKS_LARGE   // staging chunks of the decode kernel for batches past kDecRound
+#define RLE_DEC_CHUNKS_LARGE 96
+#endif
+constexpr uint32_t kDecChunksLarge = RLE_DEC_CHUNKS_LARGE;
 bool dec_order_enabled() {
     static const bool on = !(getenv("RLE_MI355X_DEC_ORDER") && !strcmp(getenv("RLE_MI355X_DEC_ORDER"), "0"));
     return on;
@@ -525,7 +535,10 @@ extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_of
         hipLaunchKernelGGL(rle::dec_order_hist_kernel, g, dim3(256), 0, s, d_in_len, n, hist);
         hipLaunchKernelGGL(rle::dec_order_scatter_kernel, g, dim3(256), 0, s, d_in_len, n, hist, cursor, order);
     }
-    hipLaunchKernelGGL(rle::decode_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
+    // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD)
+    auto kern = n > kDecRound && kDecChunksLarge != rle::kDecChunks ? rle::decode_kernel<kDecChunksLarge>
+                                                                    : rle::decode_kernel<rle::kDecChunks>;
+    hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
                        d_status, n, store_policy(n, false), (const uint32_t*)order);
     if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;

@@ -216,3 +216,23 @@ def test_single_value_tiles_decode_match_oracle():
         for i, y in enumerate(ys):
             ref, _ = O.decode(y, us[i])
             assert dec[i] == ref, (delta, i, len(xs[i]))
+
+
+def test_large_batch_small_staging_matches_oracle():
+    """Batches past one residency round (> 4096 buffers) decode with the 96-chunk staging
+    (csrc/rle_kernels.hip decode_kernel<kDecChunksLarge>), where output-heavy general tiles (runs of
+    mixed values) stage in two passes: every data kind, ragged sizes, bit-exact."""
+    from test_gpu_parity import _oracle_parity
+    rng = np.random.default_rng(21)
+    xs = []
+    for i in range(4400):
+        kind = i % 6
+        n = int(rng.integers(1, 9000))
+        if kind < 4:
+            xs.append(O.gen(kind, 7000 + i, n))
+        elif kind == 4:   # runs of 8-9 of changing values: ~2.9x expansion, not single-valued
+            lens = rng.integers(8, 10, size=n // 8 + 2)
+            xs.append(np.repeat(rng.integers(0, 256, size=len(lens)).astype(np.uint8), lens)[:n].tobytes())
+        else:
+            xs.append(_pairs_data(rng, n, 0.05))
+    _oracle_parity(xs)

@@ -24,7 +24,8 @@ PROF = os.path.join(REPO, "profiles")
 
 
 def short(name):
-    return name.split("(")[0].replace("rle::", "").replace("void ", "")
+    # template arguments dropped: decode_kernel<96u> / <192u> (the staging size) are one kernel
+    return name.split("(")[0].split("<")[0].replace("rle::", "").replace("void ", "")
 
 
 def kernel_split(src):
