@@ -100,9 +100,10 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     tl_mark(b, 0, lane);
     tl_put(b, 13, tl0, lane);
     tl_ids(b, lane);
-    const uint64_t U64 = in_len[b];
-    const uint8_t* src = in + in_off[b];
-    uint8_t* dst = out + out_off[b];
+    const uint64_t U64 = in_len[b], ioff = in_off[b], ooff = out_off[b];
+    __builtin_amdgcn_sched_barrier(0);   // the three loads in flight together (as in decode_kernel)
+    const uint8_t* src = in + ioff;
+    uint8_t* dst = out + ooff;
     u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
     if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
     if (bad) {
@@ -306,9 +307,12 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     tl_put(b, 13, tl0, lane);
     tl_ids(b, lane);
     const uint64_t* capp = out_cap ? out_cap : out_len;
-    const uint64_t C64 = in_len[bi], U64 = out_len[bi], cap = capp[bi];
-    const uint8_t* src = in + in_off[bi];
-    uint8_t* dst = out + out_off[bi];
+    const uint64_t C64 = in_len[bi], U64 = out_len[bi], cap = capp[bi], ioff = in_off[bi], ooff = out_off[bi];
+    // all five loads in flight before the first use (else hipcc waits for in_off before issuing the
+    // other four: two memory round trips ahead of the first tile's DMA instead of one)
+    __builtin_amdgcn_sched_barrier(0);
+    const uint8_t* src = in + ioff;
+    uint8_t* dst = out + ooff;
     u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
     if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
     const u32 C = (u32)C64, U = (u32)U64;
