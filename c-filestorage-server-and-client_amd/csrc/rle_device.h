@@ -18,9 +18,12 @@
 // stores sits in the loop.  Run boundaries and token starts are 16-bit per-lane masks from SWAR
 // byte compares; the sequential state (encode: run start position; decode: token phase 0..2 as a
 // v_perm byte map) and output offsets cross lanes by DPP wave scans and cross tiles in scalar
-// registers.  Each lane scatters its output into a per-wave LDS staging area that is linear per
-// tile, and complete 16-byte chunks leave as coalesced buffer_store_dwordx4.  No MFMA: this is an
-// HBM-bound byte scan.
+// registers.  In the general path each lane scatters its output into a per-wave LDS staging area
+// that is linear per tile, and complete 16-byte chunks leave as coalesced buffer_store_dwordx4.
+// Tiles of common shapes skip the staging: literal tiles (runs <= 2: each
+// lane's output is its bytes with <= 2 removed or inserted, one v_perm per dword, stored as
+// unaligned 16-byte stores), encoder run tiles (a 3-periodic "v v 9" pattern) and decoder
+// single-value tiles (rep4(v) chunks).  No MFMA: this is an HBM-bound byte scan.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
