@@ -318,13 +318,19 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const u32 C = (u32)C64, U = (u32)U64;
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     const u32 ntiles = (b < n && !bad && !RLE_NOWALK) ? ntiles_for(C) : 0u;
+    tl_mark(b, 14u + 0u * ntiles, lane);   // (diagnostic builds: the metadata has arrived)
     uint8_t* stage = stage_all + wid * kStageB;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    // The phase table and the compaction selectors: every wave with tiles to walk LDS-DMAs both
-    // into the workgroup's copy (the same bytes, so the waves' writes agree) ahead of its first
-    // tile's load.  Loads complete in issue order, so walk_tiles' wait for tile 0 covers them and no
-    // barrier is needed; a wave without tiles issues none (nothing may land after it ends).
-    if (ntiles) {
+    // The phase table and the compaction selectors, shared by the workgroup: wave 0 LDS-DMAs them
+    // (2.3 KB) after every wave has issued its first tiles' loads, waits for its own table loads
+    // (they complete in issue order, its tile loads after them may still be in flight), and one
+    // barrier publishes them, normally before the first tile's data has landed.  (At kernel start
+    // every wave's loads queue at once: one copy per workgroup instead of per wave keeps the
+    // table traffic off the first tiles' path.)
+    stagger();
+    walk_prime(rsi, 0u, ntiles, lane, slots);
+    tl_mark(b, 15, lane);   // (diagnostic builds: the first tiles' loads issued)
+    if (wid == 0u) {
         const u32x4 rt = make_rsrc(&kDecTable, (u32)sizeof(DecTable));
         const u32 lt = uniform(lds_addr(tbl));
         asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
@@ -333,11 +339,11 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         if (lane < kCompactEntries)
             dma_tile(make_rsrc(&kCompactLut, (u32)sizeof(DecCompactLut)), 16u * lane, uniform(lds_addr(clut)));
     }
-    stagger();
-    walk_prime(rsi, 0u, ntiles, lane, slots);
     for (u32 k = lane; k < kStageB / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
-    wave_lds_sync();
+    if (wid == 0u) vm_drain();   // (its own tile loads were issued first: both are in)
+    if (kDecWaves > 1) __syncthreads();
+    else wave_lds_sync();
 
     if (b < n) {
         if (bad) {

@@ -66,6 +66,12 @@ def report(name, tl, n):
     last = np.where(tl[:, 2:10] > 0, tl[:, 2:10], 0).max(axis=1)
     print(f"  last tile -> end {pct((tl[:, 10] - last) / 100.0)}")
     print(f"  entry -> tile0 {pct((tl[:, 2] - tl[:, 0]) / 100.0)}")
+    if (tl[:, 14] > 0).any():   # decode: metadata arrival and first loads issued
+        m = (tl[:, 14] > 0) & (tl[:, 15] > 0)
+        print(f"  entry -> metadata {pct((tl[m, 14] - tl[m, 0]) / 100.0)}")
+        print(f"  metadata -> loads issued {pct((tl[m, 15] - tl[m, 14]) / 100.0)}")
+        print(f"  loads issued -> walk start {pct((tl[m, 1] - tl[m, 15]) / 100.0)}")
+        print(f"  walk start -> tile0 {pct((tl[m, 2] - tl[m, 1]) / 100.0)}")
     xcc = tl[:, 12] & 0xF
     hw = tl[:, 11]
     # per SIMD (XCC, SE, SH, CU, SIMD from HW_ID): tiles walked by its waves, and its last end
