@@ -173,6 +173,14 @@ __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v, bool wt) {
     else
         asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
+// One 4-byte store (buffer_store_dword; offsets need not be aligned).
+__device__ __forceinline__ void vstore4(u32x4 rs, u32 voff, u32 v, bool wt) {
+    if (wt)
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+    else
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+
 // wait until at most n vector-memory ops are outstanding
 #define RLE_VMW(N)                                            \
     case N:                                                   \
@@ -553,24 +561,33 @@ constexpr EncInsLut make_ins_lut() {
 static __constant__ EncInsLut kEncInsLut = make_ins_lut();
 
 // Returns the store instructions issued, or kNotFast (nothing done: the general path encodes the
-// tile).  Only for tiles before the last one, with st.head == 0.
-template <bool k64>
+// tile).  With st.head == 0.  kTail: the buffer's last tile (positions past U are neither tokens
+// nor output).  Its output ends the stream at C = out_pos + ttot, so its stores go through a
+// descriptor clipped at C (the range check drops dwords not wholly below it: nothing lands past
+// C), and the last 4 output bytes are stored again as one dword ending at C, as in decode.
+template <bool k64, bool kTail = false>
 __device__ __forceinline__ u32 enc_tile_fast(const EncAn& a, const uint2 look, u32 pos, u32 lane, const u32* elut,
                                              uint8_t* stage, u32x4 rso, EncState& st) {
     constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;
-        const bool owned = k64 || lane < kOwnLanes;
+    const bool owned = k64 || lane < kOwnLanes;
     // continuations (bit j: byte j equals byte j-1) of the lane's 16 positions and the next lane's
     // first two; pairs: run starts whose run continues
     // (runs of 3+ first, in as few instructions as possible: run-heavy tiles leave here)
     const u32 C18 = ~a.B24 & 0x3FFFFu;
     if (__builtin_amdgcn_ballot_w64(((C18 & (C18 >> 1)) != 0u) && owned)) return kNotFast;
-    const u32 P = a.B & ~(a.B24 >> 1) & 0xFFFFu;
+    const u32 vm = kTail ? a.validm : 0xFFFFu;   // positions below U (positions past U are boundaries)
+    const u32 P = a.B & ~(a.B24 >> 1) & vm;
     if (__builtin_amdgcn_ballot_w64(__builtin_popcount(P) > 2 && owned)) return kNotFast;
     if ((readlane(C18, 0) & 1u) && st.rs + 1u != pos) return kNotFast;   // the run entering is longer
     const u32 del0 = C18 & 1u;
-    const u32 nout = owned ? 16u - del0 + ((P >> 15) & 1u) + (u32)__builtin_popcount(P) : 0u;
+    const u32 nout = owned ? (u32)__builtin_popcount(vm) - del0 + ((P >> 15) & 1u) + (u32)__builtin_popcount(P) : 0u;
     const u32 oincl = wave_scan_incl(nout, 0u, OpAdd());
     const u32 ttot = readlane(oincl, 63);
+    if (kTail) {
+        if (ttot < 4u) return kNotFast;
+        rso.z = uniform(st.out_pos + ttot);   // clip every store of this tile at C
+        asm volatile("s_nop 4" ::: "memory");   // (the descriptor word is fresh)
+    }
 
     u32 rounds = 0;
     const u32 rel0 = st.out_pos - st.flushed;
@@ -620,6 +637,20 @@ __device__ __forceinline__ u32 enc_tile_fast(const EncAn& a, const uint2 look, u
         vb.x = alignbyte(out[1], out[0], b); vb.y = alignbyte(out[2], out[1], b);
         vb.z = alignbyte(out[3], out[2], b); vb.w = alignbyte(out[4], out[3], b);
         vstore(rso, nout > 16u ? o + b : kOOB, vb, st.wt);
+        ++rounds;
+    }
+    if (kTail) {
+        // the last 4 bytes of each lane's output (n >= 15 on full lanes; with n < 4, the end of the
+        // full lane before it first), stored by the last lane with output as a dword ending at C
+        const u32 s4b = nout - 4u, qd = s4b >> 2;
+        const u32 lo = qd == 0u ? out[0] : qd == 1u ? out[1] : qd == 2u ? out[2] : out[3];
+        const u32 hi = qd == 0u ? out[1] : qd == 1u ? out[2] : qd == 2u ? out[3] : out[4];
+        const u32 T4 = alignbyte(hi, lo, s4b & 3u);
+        const u32 Tp = from_prev_lane(T4, 0u);
+        const u32 T = nout >= 4u ? T4 : alignbyte(out[0], Tp, nout);
+        const uint64_t has = __builtin_amdgcn_ballot_w64(nout != 0u);
+        const u32 last = 63u - (u32)__builtin_clzll(has);
+        vstore4(rso, lane == last ? st.out_pos + ttot - 4u : kOOB, T, st.wt);
         ++rounds;
     }
     st.out_pos += ttot;
@@ -719,11 +750,16 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     const uint2 look = k64 ? *reinterpret_cast<const uint2*>(cslot + kSlot) : uint2{0u, 0u};
     next();   // the slot is free once read
     EncAn an = enc_analyze_bounds<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, kc);
-    if (kFast && RLE_ENC_FAST && !st.head && pos + (k64 ? kEncStep : kTileStep) < Uo) {
-        u32 r = enc_tile_run<k64>(an, pos, lane, stage, rso, st);
-        if (r != kNotFast) return r;
-        r = enc_tile_fast<k64>(an, look, pos, lane, elut, stage, rso, st);
-        if (r != kNotFast) return r;
+    if (kFast && RLE_ENC_FAST && !st.head) {
+        if (pos + (k64 ? kEncStep : kTileStep) < Uo) {
+            u32 r = enc_tile_run<k64>(an, pos, lane, stage, rso, st);
+            if (r != kNotFast) return r;
+            r = enc_tile_fast<k64>(an, look, pos, lane, elut, stage, rso, st);
+            if (r != kNotFast) return r;
+        } else if (Uo == Ud) {   // the buffer's last tile (not a segment's)
+            const u32 r = enc_tile_fast<k64, true>(an, look, pos, lane, elut, stage, rso, st);
+            if (r != kNotFast) return r;
+        }
     }
     enc_tokens(an, st.rs);
     constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;   // the tile's last owning lane
@@ -1204,14 +1240,6 @@ constexpr DecCompactLut make_compact_lut() {
     return t;
 }
 static __constant__ DecCompactLut kCompactLut = make_compact_lut();
-
-// One 4-byte store (buffer_store_dword; offsets need not be aligned).
-__device__ __forceinline__ void vstore4(u32x4 rs, u32 voff, u32 v, bool wt) {
-    if (wt)
-        asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
-    else
-        asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
-}
 
 // Returns the store instructions issued, or kNotFast (nothing done: the general path decodes the
 // tile).  Not for a segment's first chunk (st.head), nor with Co < C (one-wave walks only).

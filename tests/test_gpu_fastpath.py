@@ -236,3 +236,24 @@ def test_large_batch_small_staging_matches_oracle():
         else:
             xs.append(_pairs_data(rng, n, 0.05))
     _oracle_parity(xs)
+
+
+def test_literal_last_tiles_encode_match_oracle():
+    """Encoder literal path on the buffer's last tile (enc_tile_fast<k64, true>: stores clipped at
+    C, the last 4 bytes stored again): every size around the tile forms' edges, pairs in the last
+    bytes, a pair ending exactly at U, and nothing written past C (the slots are poisoned)."""
+    from test_gpu_parity import _oracle_parity
+    rng = np.random.default_rng(33)
+    xs = []
+    for n in list(range(1, 80)) + [1024 * k + d for k in range(1, 5) for d in range(-6, 7)] + \
+            [17000 + 1008 * k + d for k in range(0, 3) for d in (-3, -1, 0, 1, 5)]:
+        for p_dup in (0.0, 0.03, 0.2):
+            x = bytearray(_pairs_data(rng, n, p_dup))
+            xs.append(bytes(x))
+            if n >= 3:   # a pair as the last two bytes, and one just before them
+                y = bytearray(x)
+                y[-1] = y[-2]
+                if n >= 4 and y[-3] == y[-2]:
+                    y[-3] ^= 0x5A
+                xs.append(bytes(y))
+    _oracle_parity(xs)
