@@ -224,9 +224,18 @@ def main():
     gathered = [torch.cuda.Event() for _ in range(2)] if world > 1 else None
     nstep = [0]
 
+    # N > 1: the exchange as one library call per step on the codec's stream (csrc/rle_dist.hip)
+    # when every rank's RCCL communicator comes up; else the torch calls below, on a side stream
+    # (host-bound: tools/exchange_cost.py)
+    xch = shard.NativeExchange(B.n, world, rank, dev) if world > 1 else None
+    if xch is not None and not xch.ok and rank == 0:
+        print(f"native exchange unavailable ({xch.error}); torch calls", file=sys.stderr)
+
     def step():
         B.encode(stream)
-        if world > 1:
+        if xch is not None and xch.ok:
+            xch.step(B.clen, stream)
+        elif world > 1:
             k = nstep[0] % 2
             nstep[0] += 1
             stream.wait_event(gathered[k])
@@ -359,10 +368,15 @@ def main():
                           "buffer_bytes": wl["size"] or "mixed 4 KiB-2 MiB",
                           "u_bytes_per_gpu": total_u // world, "c_bytes_rank0": c_bytes,
                           "parallelism": f"shard round-robin over {world} GPU(s)" +
-                                         (", RCCL all-gather of sizes" if world > 1 else "")},
+                                         (", RCCL all-gather of sizes" if world > 1 else "") +
+                                         ((" (one library call per step)" if xch.ok else " (torch calls)")
+                                          if xch is not None else "")},
                "verified_bit_exact_roundtrip": ok, "kernels": kern, "roofline": roofline, "cpu_baseline": cpu,
                "north_star_dec64k": north, "concurrent_streams": conc}
         print(json.dumps(out))
+    if xch is not None:
+        torch.cuda.synchronize()
+        xch.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -90,6 +90,13 @@ def lib():
     L.RLEdecompressN.argtypes = [sz, vp, vp, vp, vp]
     L.rle_append_prepare_device.restype = ctypes.c_int
     L.rle_append_prepare_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp]
+    for f, a in (("rle_dist_unique_id", [vp, sz, ctypes.c_char_p]),
+                 ("rle_dist_init", [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+                 ("rle_dist_gather_offsets", [vp, u32, vp, vp, vp]),
+                 ("rle_dist_offsets_device", [vp, u32, u32, vp, vp]),
+                 ("rle_dist_finalize", [])):
+        getattr(L, f).restype = ctypes.c_int
+        getattr(L, f).argtypes = a
     _lib = L
     return L
 
@@ -279,3 +286,43 @@ def dropin_stats(reset=False) -> dict:
     if rc != RLE_OK:
         raise RLEError(f"rle_mi355x_dropin_stats failed: {rc}")
     return st.as_dict()
+
+
+# ------------------------------------------------------------------ multi-GPU exchange (csrc/rle_dist.hip)
+def _check(rc, what):
+    if rc != RLE_OK:
+        raise RLEError(f"{what} failed: {rc}")
+
+
+def _torch_rccl_path():
+    """torch's own librccl (the copy torch.distributed's "nccl" backend loaded), so the exchange uses
+    the same RCCL library as the process group."""
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p.encode() if os.path.exists(p) else None
+
+
+def dist_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().rle_dist_unique_id(buf, 128, _torch_rccl_path()), "rle_dist_unique_id")
+    return buf.raw
+
+
+def dist_init(uid: bytes, rank: int, world: int):
+    _check(lib().rle_dist_init(uid, len(uid), rank, world, _torch_rccl_path()), "rle_dist_init")
+
+
+def dist_gather_offsets(sizes, gathered, offsets, stream=None):
+    """One exchange step (rle_dist_gather_offsets) on `stream`: sizes (int64[n], device) all-gathered
+    and scanned into offsets (int64[world * n]) in the global stream order."""
+    _check(lib().rle_dist_gather_offsets(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets),
+                                         _stream_ptr(stream)), "rle_dist_gather_offsets")
+
+
+def dist_offsets(gathered, world: int, n: int, offsets, stream=None):
+    _check(lib().rle_dist_offsets_device(_ptr(gathered), world, n, _ptr(offsets), _stream_ptr(stream)),
+           "rle_dist_offsets_device")
+
+
+def dist_finalize():
+    _check(lib().rle_dist_finalize(), "rle_dist_finalize")

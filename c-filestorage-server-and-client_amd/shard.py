@@ -37,3 +37,50 @@ def global_offsets(local_sizes: torch.Tensor, world: int) -> torch.Tensor:
 def my_offsets(glob_offsets: torch.Tensor, rank: int, world: int) -> torch.Tensor:
     """This rank's buffers' offsets in the global stream."""
     return glob_offsets[rank::world]
+
+
+class NativeExchange:
+    """global_offsets as one library call per step (rle_dist_gather_offsets, csrc/rle_dist.hip):
+    the sizes all-gathered over RCCL and scanned on the codec's stream.  The same exchange issued as
+    torch calls on a side stream costs 56-87 us of host time per configs[1] step against ~21 us of
+    GPU time (tools/exchange_cost.py).  Collective setup: every rank constructs it; rank 0's
+    communicator id is broadcast over the process group.  `ok` is False on every rank unless every
+    rank's communicator came up (then callers use global_offsets)."""
+
+    def __init__(self, n: int, world: int, rank: int, dev):
+        import rle_mi355x as R
+        self.R, self.n, self.world, self.ok = R, n, world, False
+        err = None
+        try:
+            uid = [R.dist_unique_id() if rank == 0 else None]
+        except Exception as e:   # no RCCL symbols: every rank learns it below
+            uid, err = [None], e
+        dist.broadcast_object_list(uid, src=0)
+        up = 0
+        if uid[0] is not None:
+            try:
+                R.dist_init(uid[0], rank, world)
+                up = 1
+            except Exception as e:
+                err = e
+        t = torch.tensor([up], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        self.ok = bool(t.item())
+        self.error = err
+        if not self.ok:
+            if up:
+                R.dist_finalize()
+            return
+        self.gathered = torch.empty(world * n, dtype=torch.int64, device=dev)
+        self.offsets = torch.empty(world * n, dtype=torch.int64, device=dev)
+
+    def step(self, local_sizes: torch.Tensor, stream) -> torch.Tensor:
+        """Issue one exchange on `stream` after the work issued on it so far; returns the offsets
+        tensor (complete in stream order)."""
+        self.R.dist_gather_offsets(local_sizes, self.gathered, self.offsets, stream)
+        return self.offsets
+
+    def close(self):
+        if self.ok:
+            self.R.dist_finalize()
+            self.ok = False

@@ -145,6 +145,27 @@ int rle_mi355x_stamps(unsigned long long* out9, int reset);
  * HW_ID, XCC_ID); RLE_E_INVAL otherwise. */
 int rle_mi355x_timeline(unsigned long long* out, int reset);
 
+/* ---- multi-GPU exchange (csrc/rle_dist.hip) -------------------------------
+ * The one exchange of a batch sharded round-robin over N GPUs (shard.py, bench.py --gpus N): each
+ * rank's per-buffer compressed sizes all-gathered over RCCL and scanned into offsets in the global
+ * stream (global buffer i = k * world + r is rank r's k-th buffer).  No reference interface: the
+ * reference server is single-host, single-process (src/server.c); this replaces the Python
+ * all_gather + cumsum of shard.global_offsets with one host call.  RCCL is resolved at run time from
+ * the process's librccl.so.1 (or rccl_path when non-NULL).
+ *   rle_dist_unique_id: a communicator id (128 bytes) on one rank, to be broadcast to all ranks.
+ *   rle_dist_init: this rank's communicator (once per process).
+ *   rle_dist_gather_offsets: on `stream`, after the work issued on it so far: all-gather
+ *     d_sizes[n] into d_gathered[world * n] (rank major), then the exclusive scan in global order
+ *     into d_offsets[world * n].
+ *   rle_dist_offsets_device: the scan alone, on `stream` (tests).
+ *   rle_dist_finalize: destroys the communicator. */
+int rle_dist_unique_id(void* out, size_t len, const char* rccl_path);
+int rle_dist_init(const void* id, size_t len, int rank, int world, const char* rccl_path);
+int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets,
+                            void* stream);
+int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world, uint32_t n, int64_t* d_offsets, void* stream);
+int rle_dist_finalize(void);
+
 /* Number of visible HIP devices (0 when none). */
 int rle_mi355x_device_count(void);
 
