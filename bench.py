@@ -42,6 +42,19 @@ def xs64(s):
     return s
 
 
+def set_host_wait(mode, device):
+    """How the host thread waits in hipDeviceSynchronize / hipStreamSynchronize: "spin"
+    (hipDeviceScheduleSpin) or "yield" (hipDeviceScheduleYield), set before the device is first
+    used; "auto" leaves the runtime's default.  Returns the mode applied (or an error note)."""
+    flags = {"spin": 1, "yield": 2}.get(mode)
+    if flags is None:
+        return "auto"
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch already loaded (same soname)
+    rc = hip.hipSetDevice(ctypes.c_int(device)) or hip.hipSetDeviceFlags(ctypes.c_uint(flags))
+    return mode if rc == 0 else f"{mode} (hipSetDeviceFlags rc={rc})"
+
+
 def mixed_size(i):
     """configs[2] size rule (same as oracle/ref_bench.c --size 0): log-uniform 4 KiB..1 MiB, half
     of them with a non-power-of-two remainder."""
@@ -206,6 +219,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    sched = set_host_wait(os.environ.get("RLE_BENCH_SCHED", "auto"), local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -371,7 +385,7 @@ def main():
                                          (", RCCL all-gather of sizes" if world > 1 else "") +
                                          ((" (one library call per step)" if xch.ok else " (torch calls)")
                                           if xch is not None else "")},
-               "verified_bit_exact_roundtrip": ok, "kernels": kern, "roofline": roofline, "cpu_baseline": cpu,
+               "verified_bit_exact_roundtrip": ok, "host_wait": sched, "kernels": kern, "roofline": roofline, "cpu_baseline": cpu,
                "north_star_dec64k": north, "concurrent_streams": conc}
         print(json.dumps(out))
     if xch is not None:

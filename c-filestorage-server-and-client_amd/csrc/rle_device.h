@@ -1178,6 +1178,9 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     return p.tail ? dec_lengths_t<true>(p, d) : dec_lengths_t<false>(p, d);
 }
 
+#ifndef RLE_SCAT_MASK   // 1: the scatter writes token starts only (interior writes exec-masked off)
+#define RLE_SCAT_MASK 0
+#endif
 // The scatter of one lane's decoded positions into the staging (2 bytes per position): endk = the
 // staging byte address of the lane's first decoded position.  u16 per position: the byte, with
 // the start flag (0x80) as the high byte: 0x80vv at a token start, an unflagged 0x00vv (ignored by
@@ -1196,10 +1199,17 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
             if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
             else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
         };
-        put(sub_byte<0>(endk, R), xk_lo);
-        put(sub_byte<1>(endk, R), xk_lo >> 16);
-        put(sub_byte<2>(endk, R), xk_hi);
-        put(sub_byte<3>(endk, R), xk_hi >> 16);
+        if (RLE_SCAT_MASK) {   // token starts only: the interior writes' lanes leave the bank conflicts
+            if ((int)(xk_lo << 16) < 0) put(sub_byte<0>(endk, R), xk_lo);
+            if ((int)xk_lo < 0) put(sub_byte<1>(endk, R), xk_lo >> 16);
+            if ((int)(xk_hi << 16) < 0) put(sub_byte<2>(endk, R), xk_hi);
+            if ((int)xk_hi < 0) put(sub_byte<3>(endk, R), xk_hi >> 16);
+        } else {
+            put(sub_byte<0>(endk, R), xk_lo);
+            put(sub_byte<1>(endk, R), xk_lo >> 16);
+            put(sub_byte<2>(endk, R), xk_hi);
+            put(sub_byte<3>(endk, R), xk_hi >> 16);
+        }
     }
 }
 
