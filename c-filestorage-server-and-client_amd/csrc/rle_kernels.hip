@@ -28,6 +28,9 @@ __device__ __forceinline__ u32 xcd_buffer(u32 wg, u32 ngrid, u32 waves, u32 wid)
 #define RLE_NOWALK 0
 #endif
 
+#ifndef RLE_DEC_PRIO   // decode wave priority by walk length (decode_kernel)
+#define RLE_DEC_PRIO 1
+#endif
 #ifndef RLE_STAGGER   // experiments: the waves sharing a SIMD start RLE_STAGGER * 64 cycles apart
 #define RLE_STAGGER 0
 #endif
@@ -319,6 +322,14 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     const u32 ntiles = (b < n && !bad && !RLE_NOWALK) ? ntiles_for(C) : 0u;
     tl_mark(b, 14u + 0u * ntiles, lane);   // (diagnostic builds: the metadata has arrived)
+    // Issue priority by walk length (log2 buckets of the tile count): where a SIMD holds waves of
+    // unequal walks, the longest are the launch's critical path, and the short ones fill their
+    // stalls.  RLE_DEC_PRIO: 0 off, 1 the one-round kernel (kChunks >= 191) only, 2 every size.
+    if (RLE_DEC_PRIO == 2 || (RLE_DEC_PRIO == 1 && kChunks >= 191u)) {
+        if (ntiles >= 32u) __builtin_amdgcn_s_setprio(3);
+        else if (ntiles >= 8u) __builtin_amdgcn_s_setprio(2);
+        else if (ntiles >= 3u) __builtin_amdgcn_s_setprio(1);
+    }
     uint8_t* stage = stage_all + wid * kStageB;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
     // The phase table and the compaction selectors, shared by the workgroup: wave 0 LDS-DMAs them
