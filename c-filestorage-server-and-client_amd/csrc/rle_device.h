@@ -167,16 +167,19 @@ __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
 // and the kernel boundary writes it back at about 6 TB/s (MI355X_MICROARCH.md, kernel boundaries):
 // 2.8 us for configs[1]'s 16.8 MB of decoded output.  Large launches store plainly, where writing
 // through measured 6-14 % slower (the launchers choose; rle_kernels.hip).
+#ifndef RLE_WT_BITS   // cache-policy bits of the write-through stores (experiments: "sc1 nt", "sc0 sc1")
+#define RLE_WT_BITS "sc1"
+#endif
 __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v, bool wt) {
     if (wt)
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen " RLE_WT_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
     else
         asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
 // One 4-byte store (buffer_store_dword; offsets need not be aligned).
 __device__ __forceinline__ void vstore4(u32x4 rs, u32 voff, u32 v, bool wt) {
     if (wt)
-        asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen " RLE_WT_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
     else
         asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
