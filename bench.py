@@ -214,6 +214,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-north-star", action="store_true")
+    ap.add_argument("--no-concurrent", action="store_true",
+                    help="skip the informational two-stream figure (profiling runs: its overlapped launches "
+                         "would enter the per-kernel averages)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -315,7 +318,7 @@ def main():
     # Informational, not `value`: the same round trips with two batches in flight on two streams, as
     # the drop-in runs when the server's worker threads (one HIP stream each) call it concurrently.
     conc = None
-    if rank == 0 and world == 1 and B.u_bytes <= (256 << 20) and args.steps > 0:
+    if rank == 0 and world == 1 and B.u_bytes <= (256 << 20) and args.steps > 0 and not args.no_concurrent:
         B2 = Batch(wl, rank, world, dev)
         B2.encode(stream)
         B2.calibrate()

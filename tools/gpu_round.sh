@@ -22,7 +22,7 @@ timeout -k 10 500 python -u $R/tools/roofline_sweep.py > $O/sweep.json 2> $O/swe
 rc=$?; echo "sweep rc=$rc" >> $O/status
 case $rc in 124|134|137|139) exit $rc;; esac
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --no-cpu > $O/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --no-cpu --no-concurrent > $O/prof.log 2>&1
 rc=$?; echo "prof rc=$rc" >> $O/status
 case $rc in 124|134|137|139) exit $rc;; esac
 for WL in cfg1 dec64k; do
