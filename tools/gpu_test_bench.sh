@@ -12,5 +12,5 @@ echo "pytest rc=$rc" | tee -a $O/status
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 timeout -k 10 400 python $R/bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "bench failed" | tee -a $O/status; exit 3; }
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --no-cpu > $O/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --no-cpu --no-concurrent > $O/prof.log 2>&1
 echo "prof rc=$?" | tee -a $O/status
