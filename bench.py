@@ -12,11 +12,18 @@ global stream offsets; payloads never leave their GPU.
 value = uncompressed bytes round-tripped by all ranks / max-over-ranks wall time of K steps.
 Default workload: BASELINE configs[1], 4096 x 4 KiB synthetic buffers per GPU (random / zero).
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1|dec64k|mixed|cfg3]
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1|dec64k|mixed|cfg3|...]
+
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N rank processes itself
+(127.0.0.1 rendezvous) before anything touches the GPU; under torch.distributed.run each rank
+reads RANK / LOCAL_RANK / WORLD_SIZE.  `--dry-run` runs the same rank loop on the CPU over gloo with
+the codec launches left out (sizes come from a closed form): it exercises the rank spawn, the
+process group, the exchange fallback, the barriers and the max-over-ranks timing, never the GPU.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -27,7 +34,7 @@ sys.path[:0] = [os.path.join(REPO, "c-filestorage-server-and-client_amd")]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-import rle_mi355x as R  # noqa: E402
+import rle_mi355x as R  # noqa: E402  (loads nothing until first use)
 import shard  # noqa: E402
 
 METRIC = "GiB/s RLE encode+decode, device-resident, batched 4–256 KiB buffers"
@@ -94,8 +101,13 @@ WORKLOADS = {
 }
 
 
+# ---------------------------------------------------------------------------------------- batches
 class Batch:
-    """One rank's shard of a synthetic batch, resident in HBM, with compressed and decoded slots."""
+    """One rank's shard of a synthetic batch, resident in HBM, with compressed and decoded slots.
+    Two compressed-size vectors alternate between steps (clens[step % 2]), so a step's size exchange
+    may still be reading its vector while the next step's encode writes the other one."""
+
+    seg = False   # True: the segmented (several waves per buffer) entry points
 
     def __init__(self, wl, rank, world, dev):
         n = wl["n"]
@@ -118,7 +130,8 @@ class Batch:
         self.u_bytes = sum(sizes)
         self.offs, self.lens = i64(offs), i64(sizes)
         self.coffs = i64(coffs)
-        self.clen = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.clens = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(2)]
+        self.clen = self.clens[0]
         self.status = torch.zeros(n, dtype=torch.int32, device=dev)
         # zero-filled, so the padding between buffers (sizes not a multiple of 16, RLE_BENCH_PAD) is
         # equal in d_in and d_out and the whole-arena comparison checks only the decoded bytes
@@ -129,22 +142,22 @@ class Batch:
         R.gen_synthetic(self.d_in, self.offs, self.lens, kind_t, i64(gidx))
         torch.cuda.synchronize()
 
-    seg = False   # True: the segmented (several waves per buffer) entry points
-
-    def encode(self, stream=None):
+    def encode(self, stream=None, slot=0):
+        clen = self.clens[slot]
         if self.seg:
-            R.encode_batch_seg(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status,
+            R.encode_batch_seg(self.d_in, self.offs, self.lens, self.d_c, self.coffs, clen, self.status,
                                total_in_bytes=self.u_bytes, workspace=self.ws_enc, stream=stream)
         else:
-            R.encode_batch(self.d_in, self.offs, self.lens, self.d_c, self.coffs, self.clen, self.status,
+            R.encode_batch(self.d_in, self.offs, self.lens, self.d_c, self.coffs, clen, self.status,
                            stream=stream, max_len=self.max_u)
 
-    def decode(self, stream=None):
+    def decode(self, stream=None, slot=0):
+        clen = self.clens[slot]
         if self.seg:
-            R.decode_batch_seg(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
+            R.decode_batch_seg(self.d_c, self.coffs, clen, self.d_out, self.offs, self.lens, None, self.status,
                                total_in_bytes=self.c_cap, workspace=self.ws_dec, stream=stream)
         else:
-            R.decode_batch(self.d_c, self.coffs, self.clen, self.d_out, self.offs, self.lens, None, self.status,
+            R.decode_batch(self.d_c, self.coffs, clen, self.d_out, self.offs, self.lens, None, self.status,
                            stream=stream, max_in_len=self.max_c, max_out_len=self.max_u)
 
     def calibrate(self):
@@ -152,7 +165,87 @@ class Batch:
         torch.cuda.synchronize()
         self.max_c = int(self.clen.max().item())
 
+    def verify(self):
+        """decode(encode(x)) == x over the whole arena and every status clean."""
+        torch.cuda.synchronize()
+        return bool(torch.equal(self.d_out, self.d_in)) and int(self.status.abs().sum().item()) == 0
 
+
+class DryBatch:
+    """--dry-run stand-in for Batch (CPU, no codec): the same shard layout, with each buffer's
+    "compressed size" a closed form of its global index, so that the exchange's offsets can be
+    checked exactly on every rank."""
+
+    seg = False
+
+    def __init__(self, wl, rank, world, dev):
+        self.n = wl["n"]
+        gidx = torch.arange(self.n, dtype=torch.int64) * world + rank
+        self.sizes_t = self.dry_sizes(gidx, wl)
+        self.clens = [torch.zeros(self.n, dtype=torch.int64) for _ in range(2)]
+        self.clen = self.clens[0]
+        self.u_bytes = self.n * (wl["size"] or 4096)
+
+    @staticmethod
+    def dry_sizes(gidx, wl):
+        U = wl["size"] or 4096
+        return (gidx * 2654435761) % (U + U // 2) + 1
+
+    def encode(self, stream=None, slot=0):
+        self.clens[slot].copy_(self.sizes_t)
+
+    def decode(self, stream=None, slot=0):
+        pass
+
+    def calibrate(self):
+        pass
+
+    def verify(self):
+        return None   # nothing was encoded
+
+
+# --------------------------------------------------------------------------------- rank spawning
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n, argv):
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE set, rendezvous on
+    127.0.0.1) and wait for them.  This process never touches the GPU.  If a rank fails, the others
+    are stopped (they would wait in a collective for it).  Returns the exit code."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                print(f"bench: a rank exited with {c}; stopping the others", file=sys.stderr)
+                for q in procs:
+                    q.terminate()
+                deadline = time.time() + 20
+                for q in procs:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+# ------------------------------------------------------------------------------------ measurement
 def time_kernels(fn, reps, stream):
     """Average duration of fn's launch: reps launches back to back on the stream the kernel runs on,
     between one pair of HIP events (an event pair around every launch would add its own dispatch,
@@ -169,14 +262,32 @@ def time_kernels(fn, reps, stream):
 
 def copy_ceiling(B, alg, reps, stream):
     """Practical ceiling: a device-to-device copy that moves the same algorithmic
-    bytes as one codec launch (alg / 2 read + alg / 2 written, HBM to HBM), timed like the kernels.
-    Runs after the round trip was verified; it overwrites the front of d_out with d_in's bytes, which
-    is the decoded content anyway."""
-    n = min(alg // 2, B.d_in.numel(), B.d_out.numel())
+    bytes as one codec launch (alg / 2 read + alg / 2 written, HBM to HBM), timed like the kernels,
+    by the library's hand-written 16-byte-per-lane streaming copy (rle_copy_device) and by the
+    runtime's hipMemcpyAsync.  Runs after the round trip was verified; it overwrites the front of
+    d_out with d_in's bytes, which is the decoded content anyway."""
+    n = min(alg // 2, B.d_in.numel(), B.d_out.numel()) & ~15
     src, dst = B.d_in[:n], B.d_out[:n]
-    t = time_kernels(lambda: dst.copy_(src), reps, stream)
+    t_k = time_kernels(lambda: R.copy_device(dst, src, n, stream), reps, stream)
+    t_r = time_kernels(lambda: dst.copy_(src), reps, stream)
+    t = min(t_k, t_r)
     return {"GBps": round(2 * n / t / 1e9, 2), "frac": round(2 * n / t / 1e9 / HBM_PEAK_GBPS, 4), "bytes": 2 * n,
-            "us": round(t * 1e6, 3), "op": "torch copy_ (hipMemcpyAsync device to device)"}
+            "us": round(t * 1e6, 3), "kernel_us": round(t_k * 1e6, 3), "memcpy_us": round(t_r * 1e6, 3),
+            "op": "the faster of rle_copy_device (16 B per lane, hand-written) and hipMemcpyAsync, device to device"}
+
+
+def step_kernels(B, reps, stream):
+    """Per-kernel durations consistent with the step: t_pair is `reps` encode+decode pairs back to
+    back between one event pair (the step's own launch pattern, no host sync in between); it is
+    split between the two kernels in the ratio of their back-to-back single-kernel times.  So the
+    two kernels sum to the step's GPU time (round 2 timed each kernel alone; their sum exceeded the
+    step by 3.5 %)."""
+    t_pair = time_kernels(lambda: (B.encode(stream), B.decode(stream)), reps, stream)
+    t_enc1 = time_kernels(lambda: B.encode(stream), reps, stream)
+    t_dec1 = time_kernels(lambda: B.decode(stream), reps, stream)
+    f = t_enc1 / (t_enc1 + t_dec1)
+    return t_pair * f, t_pair * (1 - f), {"pair_us": t_pair * 1e6, "encode_alone_us": t_enc1 * 1e6,
+                                         "decode_alone_us": t_dec1 * 1e6}
 
 
 def cpu_baseline(wl, seconds, threads, flavor):
@@ -205,7 +316,363 @@ def load_pmc(workload):
         return None
 
 
-def main():
+# ------------------------------------------------------------------------------------ the exchange
+class Exchange:
+    """The N > 1 exchange step of one rank: after a step's encode, its compressed
+    sizes are all-gathered and scanned into global stream offsets.  Modes (RLE_BENCH_XMODE):
+      async    (default) one library call per step (rle_dist_gather_offsets_async): the gather +
+               scan run on a side stream after the step's encode, beside its decode and the next
+               step's encode; the codec stream waits only for the previous step's exchange;
+      inline   one library call (rle_dist_gather_offsets: ncclAllGather + the scan kernels) on the
+               codec's stream, between encode and decode;
+      graph    the inline calls captured with the whole timed loop in one HIP graph, the gather of
+               step i on a graph branch beside decode i and encode i + 1;
+      torch    shard.global_offsets (all_gather_into_tensor + cumsum) on a side stream: the fallback
+               when RCCL cannot be resolved on every rank, and the --dry-run (gloo, CPU) path.
+    Every rank takes the same mode (flags all-reduced with MIN before any rank commits)."""
+
+    def __init__(self, B, world, rank, dev, dry, xmode):
+        self.B, self.world, self.rank, self.dev, self.dry = B, world, rank, dev, dry
+        self.mode, self.error, self.xch = "torch", None, None
+        self.nstep = 0
+        if not dry:
+            self.comm = torch.cuda.Stream(device=dev)
+            self.gathered = [torch.cuda.Event() for _ in range(2)]
+            try:
+                self.xch = shard.NativeExchange(B.n, world, rank, dev)
+                if self.xch.ok:
+                    self.mode = xmode
+                else:
+                    self.error = self.xch.error
+            except Exception as e:   # every rank reaches the collective checks inside NativeExchange
+                self.error = e
+        self.offsets = None
+
+    def run(self, stream, slot):
+        """One exchange on the sizes of clens[slot], after the encode issued on `stream`."""
+        clen = self.B.clens[slot]
+        if self.mode in ("inline", "graph"):
+            self.offsets = self.xch.step(clen, stream, slot)
+        elif self.mode == "async":
+            self.offsets = self.xch.step_async(clen, stream, self.comm, slot)
+        elif self.dry:
+            self.offsets = shard.global_offsets(clen, self.world)
+        else:
+            k = slot
+            self.comm.wait_stream(stream)
+            with torch.cuda.stream(self.comm):
+                self.offsets = shard.global_offsets(clen, self.world)
+                self.gathered[k].record(self.comm)
+
+    def verify(self, stream):
+        """Once, before timing: this rank's exchange result for clens[0] against the torch
+        process-group path (shard.global_offsets) -- exact int64 equality."""
+        if not self.dry:
+            torch.cuda.synchronize()
+        ref = shard.global_offsets(self.B.clens[0], self.world)
+        if self.dry:
+            n, w = self.B.n, self.world
+            gidx = torch.arange(n * w, dtype=torch.int64)
+            s = DryBatch.dry_sizes(gidx, {"size": self.B.u_bytes // n})
+            ok = torch.equal(ref, torch.cumsum(s, 0) - s)
+        else:
+            torch.cuda.synchronize()
+            ok = torch.equal(self.offsets, ref)
+        return bool(ok)
+
+    def close(self):
+        if self.xch is not None:
+            if not self.dry:
+                torch.cuda.synchronize()
+            self.xch.close()
+
+
+# ----------------------------------------------------------------------------------- the rank loop
+class Loop:
+    """The timed loop of one rank: `steps(k)` issues k steps (eager), or replays a captured graph
+    of k steps (Exchange mode "graph").  In graph mode step i encodes into clens[i % 2]; the gather of
+    step i runs on a branch, beside decode i and encode i + 1, and encode i + 2 (which rewrites
+    clens[i % 2]) waits for it."""
+
+    def __init__(self, B, xch, stream, dry):
+        self.B, self.xch, self.stream, self.dry = B, xch, stream, dry
+        self.graphs = {}
+
+    def one_step(self, slot):
+        if self.xch is not None and self.xch.mode == "torch" and not self.dry:
+            self.stream.wait_event(self.xch.gathered[slot])   # the side-stream gather still reading clens[slot]
+        self.B.encode(self.stream, slot)
+        if self.xch is not None:
+            self.xch.run(self.stream, slot)
+        self.B.decode(self.stream, slot)
+
+    def _issue_pipelined(self, k, main, side):
+        done = [None, None]
+        for i in range(k):
+            slot = i % 2
+            if done[slot] is not None:
+                main.wait_event(done[slot])
+            self.B.encode(main, slot)
+            enc = torch.cuda.Event()
+            enc.record(main)
+            side.wait_event(enc)
+            self.xch.run(side, slot)
+            done[slot] = torch.cuda.Event()
+            done[slot].record(side)
+            self.B.decode(main, slot)
+        main.wait_stream(side)
+
+    def capture(self, k):
+        g = torch.cuda.CUDAGraph()
+        main = torch.cuda.Stream(device=self.stream.device)
+        side = torch.cuda.Stream(device=self.stream.device)
+        main.wait_stream(self.stream)
+        with torch.cuda.graph(g, stream=main, capture_error_mode="relaxed"):
+            side.wait_stream(main)
+            self._issue_pipelined(k, main, side)
+        self.stream.wait_stream(main)
+        torch.cuda.synchronize()
+        self.graphs[k] = g
+
+    def steps(self, k):
+        if self.xch is not None and self.xch.mode == "graph":
+            if k not in self.graphs:
+                self.capture(k)
+            self.graphs[k].replay()
+            return
+        for i in range(k):
+            self.one_step(i % 2)
+
+
+def sync(dry):
+    if not dry:
+        torch.cuda.synchronize()
+
+
+def run_rank(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dry = args.dry_run
+    wl = WORKLOADS[args.workload]
+    # RLE_BENCH_FORCE_EXCHANGE=1 (rehearsal on a one-GPU box): a one-rank process group and the whole
+    # N > 1 path -- RCCL communicator, exchange, graph capture, barriers -- at world size 1
+    multi = world > 1 or os.environ.get("RLE_BENCH_FORCE_EXCHANGE") == "1"
+    if multi:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+    if dry:
+        dev, sched, stream = torch.device("cpu"), "n/a (dry run)", None
+        if os.environ.get("RLE_BENCH_DRY_FAIL_RANK") == str(rank):   # tests: a rank that dies before the rendezvous
+            sys.exit(3)
+        if multi:
+            dist.init_process_group("gloo")
+        B = DryBatch(wl, rank, world, dev)
+    else:
+        sched = set_host_wait(os.environ.get("RLE_BENCH_SCHED", "auto"), local)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if multi:
+            dist.init_process_group("nccl", device_id=dev)
+        stream = torch.cuda.current_stream()
+        B = Batch(wl, rank, world, dev)
+
+    xmode = os.environ.get("RLE_BENCH_XMODE", "async")
+    if xmode not in ("async", "inline", "graph"):
+        raise SystemExit(f"RLE_BENCH_XMODE={xmode}: async, inline or graph")
+    xch = Exchange(B, world, rank, dev, dry, xmode) if multi else None
+    if xch is not None and xch.mode == "torch" and not dry and rank == 0:
+        print(f"native exchange unavailable ({xch.error}); torch calls", file=sys.stderr)
+    loop = Loop(B, xch, stream, dry)
+
+    B.encode(stream)
+    B.calibrate()
+    # verified on one step first, so that the W warmup steps run right before the timed region (host
+    # work between them, with the GPU idle, made the first timed step ~50 us slower: tools/step_profile.py)
+    loop.one_step(0)
+    sync(dry)
+    ok = B.verify()
+    offsets_ok = xch.verify(stream) if xch is not None else None
+    c_bytes = int(B.clen.sum().item())
+    u_local = B.u_bytes
+    # the graph (N > 1) is captured here, outside the timed region, and replayed for warmup too
+    graph_ok = None
+    if xch is not None and xch.mode == "graph":
+        try:
+            loop.capture(args.steps)
+            if args.warmup != args.steps:
+                loop.capture(max(1, args.warmup))
+            up = 1
+        except Exception as e:
+            print(f"rank {rank}: graph capture failed ({e}); eager exchange", file=sys.stderr)
+            up = 0
+        t = torch.tensor([up], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        graph_ok = bool(t.item())
+        if not graph_ok:
+            xch.mode = "inline"
+            loop.graphs.clear()
+    loop.steps(max(1, args.warmup))
+
+    if multi:
+        dist.barrier()
+    sync(dry)
+    t0 = time.perf_counter()
+    loop.steps(args.steps)
+    sync(dry)
+    if multi:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if multi:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0, 1 if offsets_ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = None if dry else bool(okt[0].item())
+        offsets_ok = bool(okt[1].item())
+        ut = torch.tensor([u_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(ut, op=dist.ReduceOp.SUM)
+        total_u = int(ut.item())
+    else:
+        total_u = u_local
+
+    kern = roofline = conc = north = cpu = None
+    if not dry:
+        kern, roofline = measure_kernels(B, args, stream, u_local, c_bytes)
+        if rank == 0 and not multi:
+            conc = concurrent_streams(B, wl, args, stream, dev)
+            if not args.no_north_star and args.workload != "dec64k":
+                loop.B = B = None   # the codec batch's HBM is released before the dec64k batch
+                torch.cuda.empty_cache()
+                north = north_star(args, stream, dev)
+            cpu = cpu_leg(wl, args, c_bytes)
+
+    if rank == 0:
+        value = total_u * args.steps / elapsed / GIB
+        par = f"shard round-robin over {world} GPU(s)"
+        if xch is not None:
+            par += {"inline": ", RCCL all-gather of sizes + scan, one library call per step on the codec stream",
+                    "async": ", RCCL all-gather of sizes + scan per step on a side stream beside the codec "
+                             "(one library call per step)",
+                    "graph": ", RCCL all-gather of sizes + scan per step on a graph branch beside the codec "
+                             "(whole timed loop captured in one HIP graph)",
+                    "torch": ", all-gather of sizes via torch.distributed (" + ("gloo" if dry else "nccl") + ")"}[xch.mode]
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+               "data": "synthetic" if not dry else "dry run: no codec launches, closed-form sizes (CPU, gloo)",
+               "config": {"workload": wl["desc"], "buffers_per_gpu": wl["n"],
+                          "buffer_bytes": wl["size"] or "mixed 4 KiB-2 MiB",
+                          "u_bytes_per_gpu": total_u // world, "c_bytes_rank0": c_bytes, "parallelism": par},
+               "verified_bit_exact_roundtrip": ok, "host_wait": sched, "kernels": kern, "roofline": roofline,
+               "cpu_baseline": cpu, "north_star_dec64k": north, "concurrent_streams": conc}
+        if xch is not None:
+            out["exchange"] = {"mode": xch.mode, "offsets_match_process_group": offsets_ok, "graph_captured": graph_ok,
+                               "error": str(xch.error) if xch.error else None}
+        if dry:
+            out["dry_run"] = True
+        print(json.dumps(out), flush=True)
+    if xch is not None:
+        loop.graphs.clear()
+        xch.close()
+    if multi:
+        dist.destroy_process_group()
+
+
+def measure_kernels(B, args, stream, u_local, c_bytes):
+    """Per-kernel durations (HIP events on the launch stream; step_kernels), algorithmic bytes =
+    U + C per launch, and the roofline object of the dominant kernel."""
+    reps = max(10, min(args.steps, 50))
+    t_enc, t_dec, detail = step_kernels(B, reps, stream)
+    alg = u_local + c_bytes
+    # GBps: algorithmic bytes (U + C) per second, the roofline numerator; U_GiBps: uncompressed bytes
+    # per second (SURVEY.md 8(d) reports both), also for the round trip
+    kern = {"encode": {"us": t_enc * 1e6, "GBps": alg / t_enc / 1e9, "U_GiBps": u_local / t_enc / GIB},
+            "decode": {"us": t_dec * 1e6, "GBps": alg / t_dec / 1e9, "U_GiBps": u_local / t_dec / GIB},
+            "roundtrip": {"us": (t_enc + t_dec) * 1e6, "U_GiBps": u_local / (t_enc + t_dec) / GIB},
+            "method": detail}
+    dom = "encode" if t_enc >= t_dec else "decode"
+    pmc = load_pmc(args.workload)
+    traffic = pmc.get(dom) if isinstance(pmc, dict) else None
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(kern[dom]["GBps"], 2), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(kern[dom]["GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "alg_bytes_per_launch": alg, "copy_ceiling": copy_ceiling(B, alg, reps, stream)}
+    return kern, roofline
+
+
+def concurrent_streams(B, wl, args, stream, dev):
+    """Informational, not `value`: the same round trips with two batches in flight on two streams, as
+    the drop-in runs when the server's worker threads (one HIP stream each) call it concurrently."""
+    if B.u_bytes > (256 << 20) or args.steps <= 0 or args.no_concurrent:
+        return None
+    B2 = Batch(wl, 0, 1, dev)
+    B2.encode(stream)
+    B2.calibrate()
+    ss = [stream, torch.cuda.Stream(device=dev)]
+    pair = [B, B2]
+    for k in range(4):
+        pair[k % 2].encode(ss[k % 2])
+        pair[k % 2].decode(ss[k % 2])
+    torch.cuda.synchronize()
+    t0c = time.perf_counter()
+    for k in range(2 * args.steps):
+        pair[k % 2].encode(ss[k % 2])
+        pair[k % 2].decode(ss[k % 2])
+    torch.cuda.synchronize()
+    dtc = time.perf_counter() - t0c
+    conc = {"streams": 2, "value": round(B.u_bytes * 2 * args.steps / dtc / GIB, 3), "unit": "GiB/s",
+            "us_per_roundtrip": round(dtc / (2 * args.steps) * 1e6, 3),
+            "verified": bool(torch.equal(B2.d_out, B2.d_in)),
+            "note": "two independent batches, each round trip on its own stream (the drop-in's per-thread "
+                    "streams); `value` is one batch after another on one stream"}
+    del B2
+    torch.cuda.empty_cache()
+    return conc
+
+
+def north_star(args, stream, dev):
+    """The north-star figure: decode of 16384 x 64 KiB (zero / random / runs50 / runs90) as GB/s of
+    (U + C) and as a fraction of 8 TB/s, beside the copy ceiling of the same bytes."""
+    N = Batch(WORKLOADS["dec64k"], 0, 1, dev)
+    N.encode(stream)
+    N.calibrate()
+    nc = int(N.clen.sum().item())
+    td = time_kernels(lambda: N.decode(stream), 20, stream)
+    te = time_kernels(lambda: N.encode(stream), 20, stream)
+    nok = bool(torch.equal(N.d_out, N.d_in))
+    nalg = N.u_bytes + nc
+    ncopy = copy_ceiling(N, nalg, 20, stream)
+    north = {"workload": WORKLOADS["dec64k"]["desc"], "decode_us": td * 1e6,
+             "decode_U_GiBps": N.u_bytes / td / GIB, "encode_U_GiBps": N.u_bytes / te / GIB,
+             "decode_GBps": nalg / td / 1e9, "decode_frac": round(nalg / td / 1e9 / HBM_PEAK_GBPS, 4),
+             "decode_frac_of_copy": round(ncopy["us"] / (td * 1e6), 4),
+             "encode_GBps": nalg / te / 1e9, "u_bytes": N.u_bytes, "c_bytes": nc, "verified": nok,
+             "copy_ceiling": ncopy}
+    del N
+    torch.cuda.empty_cache()
+    return north
+
+
+def cpu_leg(wl, args, c_bytes):
+    if args.no_cpu:
+        return None
+    threads = min(16, os.cpu_count() or 1)
+    r0 = cpu_baseline(wl, args.cpu_seconds, threads, "O0")
+    r2 = cpu_baseline(wl, max(2.0, args.cpu_seconds / 2), threads, "O2")
+    if not r0:
+        return None
+    return {"value": round(r0["rt_gibs"], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "sample": f"reference src/rleCompression.c compiled unchanged with its Makefile flags "
+                      f"(-Wall -g -std=c99), {threads} pthreads, repeated passes over the same batch for "
+                      f"{args.cpu_seconds:.0f} s ({r0['buffers']} buffers, {r0['u_bytes']} bytes)",
+            "c_batch_match": r0["c_batch"] == c_bytes,
+            "O2": round(r2["rt_gibs"], 4) if r2 else None}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -217,185 +684,19 @@ def main():
     ap.add_argument("--no-concurrent", action="store_true",
                     help="skip the informational two-stream figure (profiling runs: its overlapped launches "
                          "would enter the per-kernel averages)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU / gloo rehearsal of the rank loop without codec launches (tests)")
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    sched = set_host_wait(os.environ.get("RLE_BENCH_SCHED", "auto"), local)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    wl = WORKLOADS[args.workload]
-    stream = torch.cuda.current_stream()
-
-    B = Batch(wl, rank, world, dev)
-    # N > 1: the one exchange step -- each step's compressed sizes all-gathered over RCCL and
-    # scanned into global stream offsets -- runs on its own stream, off the codec's critical path.
-    # The sizes are copied into one of two buffers, so a gather may overlap the decode of its own
-    # step and the whole next step; a step waits only for the gather of two steps back (buffer
-    # reuse).  Every gather still completes inside the timed region (the final synchronize).
-    comm = torch.cuda.Stream(device=dev) if world > 1 else None
-    sizes = [torch.empty_like(B.clen) for _ in range(2)] if world > 1 else None
-    gathered = [torch.cuda.Event() for _ in range(2)] if world > 1 else None
-    nstep = [0]
-
-    # N > 1: the exchange as one library call per step on the codec's stream (csrc/rle_dist.hip)
-    # when every rank's RCCL communicator comes up; else the torch calls below, on a side stream
-    # (host-bound: tools/exchange_cost.py)
-    xch = shard.NativeExchange(B.n, world, rank, dev) if world > 1 else None
-    if xch is not None and not xch.ok and rank == 0:
-        print(f"native exchange unavailable ({xch.error}); torch calls", file=sys.stderr)
-
-    def step():
-        B.encode(stream)
-        if xch is not None and xch.ok:
-            xch.step(B.clen, stream)
-        elif world > 1:
-            k = nstep[0] % 2
-            nstep[0] += 1
-            stream.wait_event(gathered[k])
-            sizes[k].copy_(B.clen)
-            comm.wait_stream(stream)
-            with torch.cuda.stream(comm):
-                shard.global_offsets(sizes[k], world)
-                gathered[k].record(comm)
-        B.decode(stream)
-
-    B.encode(stream)
-    B.calibrate()
-    # verified on one step first, so that the W warmup steps run right before the timed region (host
-    # work between them, with the GPU idle, made the first timed step ~50 us slower: tools/step_profile.py)
-    step()
-    torch.cuda.synchronize()
-    ok = bool(torch.equal(B.d_out, B.d_in)) and int(B.status.abs().sum().item()) == 0
-    c_bytes = int(B.clen.sum().item())
-    u_local = B.u_bytes
-    for _ in range(max(1, args.warmup)):
-        step()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
-        ut = torch.tensor([u_local], dtype=torch.int64, device=dev)
-        dist.all_reduce(ut, op=dist.ReduceOp.SUM)
-        total_u = int(ut.item())
-    else:
-        total_u = u_local
-
-    # per-kernel durations (HIP events on the launch stream), algorithmic bytes = U + C per launch
-    reps = max(10, min(args.steps, 50))
-    t_enc = time_kernels(lambda: B.encode(stream), reps, stream)
-    t_dec = time_kernels(lambda: B.decode(stream), reps, stream)
-    alg = u_local + c_bytes
-    # GBps: algorithmic bytes (U + C) per second, the roofline numerator; U_GiBps: uncompressed bytes
-    # per second (SURVEY.md 8(d) reports both), also for the round trip
-    kern = {"encode": {"us": t_enc * 1e6, "GBps": alg / t_enc / 1e9, "U_GiBps": u_local / t_enc / GIB},
-            "decode": {"us": t_dec * 1e6, "GBps": alg / t_dec / 1e9, "U_GiBps": u_local / t_dec / GIB},
-            "roundtrip": {"us": (t_enc + t_dec) * 1e6, "U_GiBps": u_local / (t_enc + t_dec) / GIB}}
-    dom = "encode" if t_enc >= t_dec else "decode"
-    pmc = load_pmc(args.workload)
-    traffic = pmc.get(dom) if isinstance(pmc, dict) else None
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(kern[dom]["GBps"], 2), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(kern[dom]["GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "alg_bytes_per_launch": alg, "copy_ceiling": copy_ceiling(B, alg, reps, stream)}
-
-    # Informational, not `value`: the same round trips with two batches in flight on two streams, as
-    # the drop-in runs when the server's worker threads (one HIP stream each) call it concurrently.
-    conc = None
-    if rank == 0 and world == 1 and B.u_bytes <= (256 << 20) and args.steps > 0 and not args.no_concurrent:
-        B2 = Batch(wl, rank, world, dev)
-        B2.encode(stream)
-        B2.calibrate()
-        ss = [stream, torch.cuda.Stream(device=dev)]
-        pair = [B, B2]
-        for k in range(4):
-            pair[k % 2].encode(ss[k % 2])
-            pair[k % 2].decode(ss[k % 2])
-        torch.cuda.synchronize()
-        t0c = time.perf_counter()
-        for k in range(2 * args.steps):
-            pair[k % 2].encode(ss[k % 2])
-            pair[k % 2].decode(ss[k % 2])
-        torch.cuda.synchronize()
-        dtc = time.perf_counter() - t0c
-        conc = {"streams": 2, "value": round(B.u_bytes * 2 * args.steps / dtc / GIB, 3), "unit": "GiB/s",
-                "us_per_roundtrip": round(dtc / (2 * args.steps) * 1e6, 3),
-                "verified": bool(torch.equal(B2.d_out, B2.d_in)),
-                "note": "two independent batches, each round trip on its own stream (the drop-in's per-thread "
-                        "streams); `value` is one batch after another on one stream"}
-        del B2
-        torch.cuda.empty_cache()
-
-    north = None
-    if rank == 0 and world == 1 and not args.no_north_star and args.workload != "dec64k":
-        del B
-        torch.cuda.empty_cache()
-        N = Batch(WORKLOADS["dec64k"], 0, 1, dev)
-        N.encode(stream)
-        N.calibrate()
-        nc = int(N.clen.sum().item())
-        td = time_kernels(lambda: N.decode(stream), 20, stream)
-        te = time_kernels(lambda: N.encode(stream), 20, stream)
-        nok = bool(torch.equal(N.d_out, N.d_in))
-        nalg = N.u_bytes + nc
-        ncopy = copy_ceiling(N, nalg, 20, stream)
-        north = {"workload": WORKLOADS["dec64k"]["desc"], "decode_us": td * 1e6,
-                 "decode_U_GiBps": N.u_bytes / td / GIB, "encode_U_GiBps": N.u_bytes / te / GIB,
-                 "decode_GBps": nalg / td / 1e9, "decode_frac": round(nalg / td / 1e9 / HBM_PEAK_GBPS, 4),
-                 "encode_GBps": nalg / te / 1e9, "u_bytes": N.u_bytes, "c_bytes": nc, "verified": nok,
-                 "copy_ceiling": ncopy}
-        del N
-        torch.cuda.empty_cache()
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
-        r0 = cpu_baseline(wl, args.cpu_seconds, threads, "O0")
-        r2 = cpu_baseline(wl, max(2.0, args.cpu_seconds / 2), threads, "O2")
-        if r0:
-            cpu = {"value": round(r0["rt_gibs"], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
-                   "sample": f"reference src/rleCompression.c compiled unchanged with its Makefile flags "
-                             f"(-Wall -g -std=c99), {threads} pthreads, repeated passes over the same batch for "
-                             f"{args.cpu_seconds:.0f} s ({r0['buffers']} buffers, {r0['u_bytes']} bytes)",
-                   "c_batch_match": r0["c_batch"] == c_bytes,
-                   "O2": round(r2["rt_gibs"], 4) if r2 else None}
-
-    if rank == 0:
-        value = total_u * args.steps / elapsed / GIB
-        out = {"metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-               "config": {"workload": wl["desc"], "buffers_per_gpu": wl["n"],
-                          "buffer_bytes": wl["size"] or "mixed 4 KiB-2 MiB",
-                          "u_bytes_per_gpu": total_u // world, "c_bytes_rank0": c_bytes,
-                          "parallelism": f"shard round-robin over {world} GPU(s)" +
-                                         (", RCCL all-gather of sizes" if world > 1 else "") +
-                                         ((" (one library call per step)" if xch.ok else " (torch calls)")
-                                          if xch is not None else "")},
-               "verified_bit_exact_roundtrip": ok, "host_wait": sched, "kernels": kern, "roofline": roofline, "cpu_baseline": cpu,
-               "north_star_dec64k": north, "concurrent_streams": conc}
-        print(json.dumps(out))
-    if xch is not None:
-        torch.cuda.synchronize()
-        xch.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if args.gpus != world:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; running {world} rank(s)", file=sys.stderr)
+    run_rank(args)
 
 
 if __name__ == "__main__":

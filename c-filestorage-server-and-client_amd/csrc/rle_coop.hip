@@ -25,6 +25,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <mutex>
+#include <unordered_map>
+
 namespace rle {
 
 constexpr u32 kCoopMaxWaves = 8;
@@ -333,15 +337,44 @@ uint32_t coop_store_policy(uint32_t n) {
     }();
     return force >= 0 ? (uint32_t)force : (n <= 4096u ? 1u : 0u);
 }
-// RLE_MI355X_COOP=0 never, =1 always (when the sizes qualify); default: when the whole launch is
-// resident at once (n x waves within kCoopWaves).  Past that the cooperative workgroups run in
-// rounds, each paying a whole buffer's setup chain, and the one-wave kernels are faster
-// (configs[1], 4096 x 4 KiB: decode 21.5 us cooperative vs 13.3 us one-wave; encode 11.9 vs 11.2).
-constexpr uint64_t kCoopWaves = 6144;   // of 8192 wave slots (256 CUs x 32)
-bool coop_enabled(uint32_t n, uint32_t waves) {
-    const char* e = getenv("RLE_MI355X_COOP");   // read per launch: tests switch it in-process
-    const int mode = e ? atoi(e) : -1;
-    return mode == 0 ? false : mode == 1 ? true : (uint64_t)n * waves <= kCoopWaves;
+// Cooperative mode: 0 never, 1 always (when the sizes qualify), -1 (default) when the whole launch is
+// resident at once.  Past one residency round the cooperative workgroups run in rounds, each paying
+// a whole buffer's setup chain, and the one-wave kernels are faster (configs[1], 4096 x 4 KiB:
+// decode 21.5 us cooperative vs 13.3 us one-wave; encode 11.9 vs 11.2).  The mode is read once from
+// RLE_MI355X_COOP; tests switch it in-process with rle_mi355x_set_coop_mode (no setenv while other
+// threads may read the environment).
+std::atomic<int> g_coop_mode{[] {
+    const char* e = getenv("RLE_MI355X_COOP");
+    return e ? atoi(e) : -1;
+}()};
+
+// Residency of one cooperative instantiation: workgroups per CU from the occupancy API (its LDS,
+// e.g. ~40-48 KB for dec_coop_kernel<W, 16384>, limits it well below the wave count), times the CUs
+// of the current device; each (kernel, device) pair is queried once.
+struct ResidencyCache {
+    std::mutex m;
+    std::unordered_map<uint64_t, uint64_t> blocks;   // key: kernel address ^ device
+} g_res;
+uint64_t resident_blocks(const void* kern, uint32_t threads) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    const uint64_t key = (uint64_t)(uintptr_t)kern ^ ((uint64_t)dev << 56);
+    std::lock_guard<std::mutex> g(g_res.m);
+    auto it = g_res.blocks.find(key);
+    if (it != g_res.blocks.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)threads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        per_cu = cus = 0;
+    }
+    const uint64_t r = (uint64_t)(per_cu > 0 ? per_cu : 0) * (uint64_t)(cus > 0 ? cus : 0);
+    g_res.blocks.emplace(key, r);
+    return r;
+}
+bool coop_admits(const void* kern, uint32_t threads, uint32_t n) {
+    const int mode = g_coop_mode.load(std::memory_order_relaxed);
+    return mode == 0 ? false : mode == 1 ? true : (uint64_t)n <= resident_blocks(kern, threads);
 }
 }  // namespace
 
@@ -352,13 +385,16 @@ extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off
                                       uint64_t max_len, void* stream) {
     if (max_len > rle::kEncStep * rle::kCoopMaxWaves || max_len <= rle::kEncStep) return 0;
     const uint32_t tiles = (uint32_t)((max_len + rle::kEncStep - 1) / rle::kEncStep);
-    if (!coop_enabled(n, tiles)) return 0;
+    if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
     const hipStream_t s = (hipStream_t)stream;
     const uint32_t wt = coop_store_policy(n);
     const dim3 g(n);
 #define RLE_ENC_COOP(W)                                                                                         \
-    hipLaunchKernelGGL(rle::enc_coop_kernel<W>, g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, d_in_len, \
-                       (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt)
+    do {                                                                                                        \
+        if (!coop_admits((const void*)rle::enc_coop_kernel<W>, 64 * W, n)) return 0;                             \
+        hipLaunchKernelGGL(rle::enc_coop_kernel<W>, g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off,     \
+                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt);                   \
+    } while (0)
     if (tiles <= 2) RLE_ENC_COOP(2);
     else if (tiles <= 3) RLE_ENC_COOP(3);
     else if (tiles <= 4) RLE_ENC_COOP(4);
@@ -376,13 +412,16 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
         max_out_len > 16384u)
         return 0;
     const uint32_t tiles = (uint32_t)((max_in_len + rle::kTileStep - 1) / rle::kTileStep);
-    if (!coop_enabled(n, tiles)) return 0;
+    if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
     const hipStream_t s = (hipStream_t)stream;
     const uint32_t wt = coop_store_policy(n);
     const dim3 g(n);
-#define RLE_DEC_COOP(W, UM)                                                                                            \
-    hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, d_in_len, \
-                       (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt)
+#define RLE_DEC_COOP(W, UM)                                                                                      \
+    do {                                                                                                         \
+        if (!coop_admits((const void*)rle::dec_coop_kernel<W, UM>, 64 * W, n)) return 0;                          \
+        hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, \
+                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt);         \
+    } while (0)
     if (max_out_len <= 4096u) {
         if (tiles <= 2) RLE_DEC_COOP(2, 4096);
         else if (tiles <= 3) RLE_DEC_COOP(3, 4096);
@@ -396,4 +435,11 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
     }
 #undef RLE_DEC_COOP
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
+}
+
+// Tests: switch the cooperative mode in-process (0 never, 1 always, -1 residency-gated default).
+extern "C" int rle_mi355x_set_coop_mode(int mode) {
+    if (mode < -1 || mode > 1) return RLE_E_INVAL;
+    g_coop_mode.store(mode, std::memory_order_relaxed);
+    return RLE_OK;
 }

@@ -14,6 +14,7 @@
 // librccl.so.1) or from an explicit path: the codec library links no second RCCL.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -54,32 +55,163 @@ bool load_rccl(const char* path) {
     return g_rccl.ok;
 }
 
-// One workgroup: thread t owns a contiguous range of the global order, sums it (gathered is rank
-// major: global i = k * world + r sits at gathered[r * n + k]), the workgroup scans the sums in
-// LDS, and each thread writes its range's exclusive offsets.
-constexpr unsigned kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void offsets_kernel(const int64_t* __restrict__ gathered, uint32_t world,
-                                                               uint32_t n, int64_t* __restrict__ out) {
-    __shared__ int64_t part[kScanThreads];
-    const uint64_t m = (uint64_t)world * n;
-    const uint64_t per = (m + kScanThreads - 1) / kScanThreads;
-    const uint64_t lo = per * threadIdx.x, hi = lo + per < m ? lo + per : m;
-    int64_t s = 0;
-    for (uint64_t i = lo; i < hi; ++i) s += gathered[(i % world) * n + i / world];
-    part[threadIdx.x] = s;
+// The reorder + exclusive scan, over the whole chip (until r3 one workgroup walked all entries on
+// one CU).  gathered is rank major -- global buffer i = k * world + r sits at gathered[r * n + k].
+// A sub-tile is T consecutive k of every rank: each rank's part is one contiguous, coalesced run,
+// and its world * T outputs are one contiguous run of the global order.  A workgroup takes `items`
+// consecutive sub-tiles, so that there are at most kMaxTiles workgroups.
+//   tile_sums_kernel   each workgroup sums its sub-tiles into ws[t];
+//   tile_scan_kernel   each workgroup adds up ws[0, t), then per sub-tile: thread j loads k = kb + j
+//                      of every rank into registers (world W a template constant up to 16), a
+//                      workgroup scan gives each k's offset, the W offsets of k go to LDS in global
+//                      order and leave as one coalesced run.
+// Small exchanges (n <= kSmallK, e.g. configs[1]'s 4096 sizes per rank) take one launch: a single
+// 512-thread workgroup walks the sub-tiles with a running carry, no workspace.  No division
+// anywhere.
+constexpr unsigned kScanThreads = 256, kSmallThreads = 512, kMaxTiles = 512;
+constexpr size_t kStageBytes = 32768;   // LDS staging of one sub-tile's outputs, at most
+constexpr uint32_t kSmallK = 8192;
+
+template <unsigned T>
+__device__ __forceinline__ int64_t block_sum(int64_t v, int64_t* red) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    __syncthreads();   // red may still be read from a previous call
+    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (unsigned d = 1; d < kScanThreads; d <<= 1) {   // inclusive Hillis-Steele scan of the sums
-        const int64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
+    int64_t s = 0;
+    for (unsigned k = 0; k < T / 64; ++k) s += red[k];
+    return s;
+}
+
+// exclusive scan over the workgroup; *total = the workgroup's sum
+template <unsigned T>
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* red, int64_t* total) {
+    const unsigned lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    int64_t x = v;
+    for (unsigned d = 1; d < 64u; d <<= 1) {
+        const int64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
     }
-    int64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (uint64_t i = lo; i < hi; ++i) {
-        const int64_t v = gathered[(i % world) * n + i / world];
-        out[i] = run;
-        run += v;
+    __syncthreads();
+    if (lane == 63u) red[w] = x;
+    __syncthreads();
+    int64_t before = 0, all = 0;
+    for (unsigned k = 0; k < T / 64; ++k) {
+        if (k < w) before += red[k];
+        all += red[k];
     }
+    *total = all;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void tile_sums_kernel(const int64_t* __restrict__ gathered, uint32_t world,
+                                                                 uint32_t n, uint32_t items, int64_t* __restrict__ ws) {
+    __shared__ int64_t red[kScanThreads / 64];
+    const uint64_t k0 = (uint64_t)blockIdx.x * items * kScanThreads;
+    const uint64_t k1 = k0 + (uint64_t)items * kScanThreads < n ? k0 + (uint64_t)items * kScanThreads : n;
+    int64_t s = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        const int64_t* g = gathered + (uint64_t)r * n;
+        for (uint64_t k = k0 + threadIdx.x; k < k1; k += kScanThreads) s += g[k];   // coalesced
+    }
+    s = block_sum<kScanThreads>(s, red);
+    if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+// W: the world size (1..16) as a constant, or 0 (any world: direct stores, no staging).  ws == NULL:
+// a single workgroup (the prefix before it is 0).
+template <unsigned W, unsigned T>
+__global__ __launch_bounds__(T) void tile_scan_kernel(const int64_t* __restrict__ gathered, uint32_t world, uint32_t n,
+                                                      uint32_t items, const int64_t* __restrict__ ws,
+                                                      int64_t* __restrict__ out) {
+    __shared__ int64_t red[T / 64];
+    __shared__ int64_t stage[W ? W * T : 1];
+    constexpr unsigned WR = W ? W : 1;
+    int64_t carry = 0;   // the sum of every workgroup's part before this one
+    {
+        int64_t pre = 0;
+        if (ws)
+            for (uint32_t t = threadIdx.x; t < blockIdx.x; t += T) pre += ws[t];
+        carry = block_sum<T>(pre, red);
+    }
+    for (uint32_t sub = 0; sub < items; ++sub) {
+        const uint64_t kb = ((uint64_t)blockIdx.x * items + sub) * T;
+        if (kb >= n) break;
+        const uint64_t k = kb + threadIdx.x;
+        const bool valid = k < n;
+        int64_t v[WR];
+        int64_t mine = 0;
+        if (W) {
+#pragma unroll
+            for (unsigned r = 0; r < WR; ++r) {
+                v[r] = valid ? gathered[(uint64_t)r * n + k] : 0;
+                mine += v[r];
+            }
+        } else if (valid) {
+            for (uint32_t r = 0; r < world; ++r) mine += gathered[(uint64_t)r * n + k];
+        }
+        int64_t total;
+        int64_t run = carry + block_excl_scan<T>(mine, red, &total);
+        if (W) {
+#pragma unroll
+            for (unsigned r = 0; r < WR; ++r) {
+                stage[threadIdx.x * WR + r] = run;
+                run += v[r];
+            }
+            __syncthreads();
+            const uint64_t cnt = (n - kb < T ? n - kb : T) * (uint64_t)WR;
+            int64_t* o = out + kb * WR;
+            for (uint64_t j = threadIdx.x; j < cnt; j += T) o[j] = stage[j];   // coalesced
+        } else if (valid) {
+            for (uint32_t r = 0; r < world; ++r) {
+                out[k * world + r] = run;
+                run += gathered[(uint64_t)r * n + k];
+            }
+        }
+        carry += total;
+    }
+}
+
+template <unsigned T>
+void launch_scan(uint32_t grid, hipStream_t s, const int64_t* g, uint32_t world, uint32_t n, uint32_t items,
+                 const int64_t* ws, int64_t* out) {
+#define RLE_SCAN(W) hipLaunchKernelGGL((tile_scan_kernel<(W * T * 8u <= kStageBytes ? W : 0u), T>), dim3(grid), dim3(T), \
+                                       0, s, g, world, n, items, ws, out)
+    switch (world) {
+        case 1: RLE_SCAN(1); break;
+        case 2: RLE_SCAN(2); break;
+        case 3: RLE_SCAN(3); break;
+        case 4: RLE_SCAN(4); break;
+        case 8: RLE_SCAN(8); break;
+        case 16: RLE_SCAN(16); break;
+        default: RLE_SCAN(0); break;
+    }
+#undef RLE_SCAN
+}
+
+// The tile sums' workspace, one per device.  It is allocated (or grown) by the first call that needs
+// it, so a caller that captures the exchange in a HIP graph makes one uncaptured call first (bench.py
+// verifies one step before it captures).
+constexpr int kMaxDevices = 64;
+int64_t* g_ws[kMaxDevices] = {};
+size_t g_ws_words[kMaxDevices] = {};
+pthread_mutex_t g_ws_lock = PTHREAD_MUTEX_INITIALIZER;
+int64_t* scan_workspace(size_t words) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    pthread_mutex_lock(&g_ws_lock);
+    if (g_ws_words[dev] < words) {
+        size_t w = g_ws_words[dev] ? g_ws_words[dev] : 4096;
+        while (w < words) w *= 2;
+        if (g_ws[dev]) (void)hipFree(g_ws[dev]);
+        g_ws[dev] = nullptr;
+        g_ws_words[dev] = 0;
+        if (hipMalloc((void**)&g_ws[dev], w * sizeof(int64_t)) == hipSuccess) g_ws_words[dev] = w;
+        else (void)hipGetLastError();
+    }
+    int64_t* p = g_ws[dev];
+    pthread_mutex_unlock(&g_ws_lock);
+    return p;
 }
 
 }  // namespace
@@ -88,10 +220,25 @@ extern "C" int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world
                                        void* stream) {
     if (!d_gathered || !d_offsets || world == 0) return RLE_E_INVAL;
     if (n == 0) return RLE_OK;
-    hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(kScanThreads), 0, (hipStream_t)stream, d_gathered, world, n,
-                       d_offsets);
+    const hipStream_t s = (hipStream_t)stream;
+    if (n <= kSmallK) {   // one launch, one workgroup
+        launch_scan<kSmallThreads>(1u, s, d_gathered, world, n, (n + kSmallThreads - 1) / kSmallThreads, nullptr,
+                                   d_offsets);
+        return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+    }
+    const uint32_t subtiles = (uint32_t)(((uint64_t)n + kScanThreads - 1) / kScanThreads);
+    const uint32_t items = (subtiles + kMaxTiles - 1) / kMaxTiles;
+    const uint32_t tiles = (subtiles + items - 1) / items;
+    int64_t* ws = scan_workspace(tiles);
+    if (!ws) return RLE_E_HIP;
+    hipLaunchKernelGGL(tile_sums_kernel, dim3(tiles), dim3(kScanThreads), 0, s, d_gathered, world, n, items, ws);
+    launch_scan<kScanThreads>(tiles, s, d_gathered, world, n, items, ws, d_offsets);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
+
+// Whether RCCL resolves in this process (bench.py's preflight: every rank checks before any rank
+// enters the blocking communicator init).
+extern "C" int rle_dist_available(const char* rccl_path) { return load_rccl(rccl_path) ? RLE_OK : RLE_E_HIP; }
 
 extern "C" int rle_dist_unique_id(void* out, size_t len, const char* rccl_path) {
     if (!out || len < sizeof(ncclUniqueId)) return RLE_E_INVAL;
@@ -124,7 +271,41 @@ extern "C" int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64
     return rle_dist_offsets_device(d_gathered, (uint32_t)g_world, n, d_offsets, stream);
 }
 
+// The exchange off the codec's stream: recorded after the encode issued on codec_stream so far, run
+// on comm_stream (gather + scan into result buffer `slot`), and the codec stream only waits -- right
+// here, before it issues the step's decode -- for the exchange of the OTHER slot, issued one call
+// earlier: so the sizes vector of that slot may be rewritten by the next step's encode.  The host
+// cost is this one call (events created once); the codec stream never waits for the gather it just
+// started.
+namespace {
+hipEvent_t g_ev_enc[2] = {}, g_ev_done[2] = {};
+bool g_done_rec[2] = {};
+}  // namespace
+extern "C" int rle_dist_gather_offsets_async(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered,
+                                             int64_t* d_offsets, void* codec_stream, void* comm_stream, int slot) {
+    if (!g_comm) return RLE_E_INVAL;
+    if (!d_sizes || !d_gathered || !d_offsets || (slot != 0 && slot != 1)) return RLE_E_INVAL;
+    for (int k = 0; k < 2; ++k) {
+        if (!g_ev_enc[k] && hipEventCreateWithFlags(&g_ev_enc[k], hipEventDisableTiming) != hipSuccess) return RLE_E_HIP;
+        if (!g_ev_done[k] && hipEventCreateWithFlags(&g_ev_done[k], hipEventDisableTiming) != hipSuccess) return RLE_E_HIP;
+    }
+    const hipStream_t cs = (hipStream_t)codec_stream, xs = (hipStream_t)comm_stream;
+    if (hipEventRecord(g_ev_enc[slot], cs) != hipSuccess || hipStreamWaitEvent(xs, g_ev_enc[slot], 0) != hipSuccess)
+        return RLE_E_HIP;
+    if (const int rc = rle_dist_gather_offsets(d_sizes, n, d_gathered, d_offsets, comm_stream)) return rc;
+    if (hipEventRecord(g_ev_done[slot], xs) != hipSuccess) return RLE_E_HIP;
+    g_done_rec[slot] = true;
+    if (g_done_rec[1 - slot] && hipStreamWaitEvent(cs, g_ev_done[1 - slot], 0) != hipSuccess) return RLE_E_HIP;
+    return RLE_OK;
+}
+
 extern "C" int rle_dist_finalize(void) {
+    for (int k = 0; k < 2; ++k) {
+        if (g_ev_enc[k]) (void)hipEventDestroy(g_ev_enc[k]);
+        if (g_ev_done[k]) (void)hipEventDestroy(g_ev_done[k]);
+        g_ev_enc[k] = g_ev_done[k] = nullptr;
+        g_done_rec[k] = false;
+    }
     int rc = RLE_OK;
     if (g_comm && g_rccl.comm_destroy(g_comm) != 0) rc = RLE_E_HIP;
     g_comm = nullptr;

@@ -106,9 +106,18 @@ constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes =
 // RLE_MI355X_STAGE_CAP=<bytes> overrides it (tests use small caps to cover the chunking).
 size_t g_stage_cap = 32u << 20;
 
-// RLE_MI355X_FAIL_ALLOC_ABOVE=<bytes> (tests only): staging / device allocations larger than that
-// fail as if memory were exhausted, so the allocation-failure paths can be exercised.
+// Test builds only (RLE_TEST_HOOKS=1: build/librle_mi355x_testhooks.so, never the product library):
+// RLE_MI355X_FAIL_ALLOC_ABOVE=<bytes> makes staging / device allocations larger than that fail as
+// if memory were exhausted, so the allocation-failure paths can be exercised.
+#ifndef RLE_TEST_HOOKS
+#define RLE_TEST_HOOKS 0
+#endif
+#if RLE_TEST_HOOKS
 size_t g_fail_above = SIZE_MAX;
+inline bool injected_failure(size_t n) { return n > g_fail_above; }
+#else
+constexpr bool injected_failure(size_t) { return false; }
+#endif
 
 struct Ctx {
     int dev = 0;
@@ -180,7 +189,9 @@ void init_once() {
         if (!strcmp(e, "pinned")) g_staging = Staging::Pinned;
         else if (!strcmp(e, "pipe")) g_staging = Staging::Pipe;
     }
+#if RLE_TEST_HOOKS
     if (const char* e = getenv("RLE_MI355X_FAIL_ALLOC_ABOVE")) g_fail_above = (size_t)strtoull(e, nullptr, 10);
+#endif
     if (const char* e = getenv("RLE_MI355X_STAGE_CAP")) {
         const long long v = atoll(e);
         if (v >= 16) g_stage_cap = (size_t)v;
@@ -236,7 +247,7 @@ void grow_host(uint8_t*& p, size_t& cap, size_t need) {
     if (p) check(hipHostFree(p), "hipHostFree");
     p = nullptr;
     cap = 0;
-    if (n > g_fail_above || hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess) {
+    if (injected_failure(n) || hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
         throw std::bad_alloc();
@@ -251,7 +262,7 @@ void grow_dev(uint8_t*& p, size_t& cap, size_t need) {
     if (p) check(hipFree(p), "hipFree");
     p = nullptr;
     cap = 0;
-    if (n > g_fail_above || hipMalloc(reinterpret_cast<void**>(&p), n) != hipSuccess) {
+    if (injected_failure(n) || hipMalloc(reinterpret_cast<void**>(&p), n) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
         throw std::bad_alloc();
@@ -811,15 +822,18 @@ struct NTotals {
     uint64_t ns_in = 0, ns_dev = 0, ns_out = 0;
 };
 
-// RLEdecompressN of one file too large for the bounded staging: straight from / to caller memory.
+// RLEdecompressN of one file too large for the bounded staging: straight from / to caller memory
+// whatever RLE_MI355X_STAGING says (the pinned and pipe modes would grow this thread's staging to
+// the file's size, which g_stage_cap exists to prevent).
 void decompress_n_alone(Ctx* c, const char* data, size_t C, size_t U, char* out, NTotals& t) {
     grow_dev(c->d_in, c->d_in_cap, round16(C));
     grow_dev(c->d_out, c->d_out_cap, round16(U));
     const uint64_t t0 = now_ns();
-    to_device(c, c->d_in, data, C);
+    check(hipMemcpyAsync(c->d_in, data, C, hipMemcpyHostToDevice, c->s), "H2D");
     const uint64_t t1 = now_ns();
     queue_decode(c, c->d_in, C, c->d_out, U, U);
-    from_device(c, out, c->d_out, U);
+    if (U) check(hipMemcpyAsync(out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     if ((uint32_t)c->h_meta[kMetaDec + 5] & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompressN");
     t.ns_in += t1 - t0;
     t.ns_dev += now_ns() - t1;

@@ -437,6 +437,30 @@ __global__ void gen_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict
     for (uint64_t q = U & ~3ull; q < U; ++q) p[q] = (uint8_t)(acc >> (8u * (uint32_t)(q & 3u)));
 }
 
+// ================================================================ streaming copy (measurement only)
+// bench.py's practical ceiling: HBM to HBM at 16 bytes per lane, four loads in
+// flight per lane before their stores, grid-strided over a chip-filling grid.  Not part of the codec.
+template <bool kNt>
+__global__ __launch_bounds__(256) void copy_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 1024u;
+    for (uint64_t base = (uint64_t)blockIdx.x * 1024u + threadIdx.x; base < n16; base += stride) {
+        u32x4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t i = base + 256u * q;
+            if (i < n16) v[q] = kNt ? __builtin_nontemporal_load(src + i) : src[i];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t i = base + 256u * q;
+            if (i < n16) {
+                if (kNt) __builtin_nontemporal_store(v[q], dst + i);
+                else dst[i] = v[q];
+            }
+        }
+    }
+}
+
 // ================================================================ DPP self-test
 __global__ void selftest_kernel(uint32_t* err) {
     __shared__ uint32_t v[64];
@@ -607,6 +631,22 @@ extern "C" int rle_gen_synthetic_device(void* d_out, const uint64_t* d_off, cons
     if (!d_out || !d_off || !d_len) return RLE_E_INVAL;
     hipLaunchKernelGGL(rle::gen_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (uint8_t*)d_out,
                        d_off, d_len, d_kind, d_index, n);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
+
+extern "C" int rle_copy_device(void* d_dst, const void* d_src, uint64_t nbytes, void* stream) {
+    if (nbytes == 0) return RLE_OK;
+    if (!d_dst || !d_src || (nbytes & 15u) || (((uintptr_t)d_dst | (uintptr_t)d_src) & 15u)) return RLE_E_INVAL;
+    const uint64_t n16 = nbytes / 16u;
+    const uint64_t want = (n16 + 1023u) / 1024u;
+    const uint32_t grid = (uint32_t)(want < 2048u ? want : 2048u);   // 8 workgroups per CU at most
+    static const bool nt = getenv("RLE_MI355X_COPY_NT") && !strcmp(getenv("RLE_MI355X_COPY_NT"), "1");
+    if (nt)
+        hipLaunchKernelGGL(rle::copy_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (rle::u32x4*)d_dst,
+                           (const rle::u32x4*)d_src, n16);
+    else
+        hipLaunchKernelGGL(rle::copy_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (rle::u32x4*)d_dst,
+                           (const rle::u32x4*)d_src, n16);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 

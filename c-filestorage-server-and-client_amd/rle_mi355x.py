@@ -90,9 +90,15 @@ def lib():
     L.RLEdecompressN.argtypes = [sz, vp, vp, vp, vp]
     L.rle_append_prepare_device.restype = ctypes.c_int
     L.rle_append_prepare_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp]
-    for f, a in (("rle_dist_unique_id", [vp, sz, ctypes.c_char_p]),
+    L.rle_mi355x_set_coop_mode.restype = ctypes.c_int
+    L.rle_mi355x_set_coop_mode.argtypes = [ctypes.c_int]
+    L.rle_copy_device.restype = ctypes.c_int
+    L.rle_copy_device.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    for f, a in (("rle_dist_available", [ctypes.c_char_p]),
+                 ("rle_dist_unique_id", [vp, sz, ctypes.c_char_p]),
                  ("rle_dist_init", [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
                  ("rle_dist_gather_offsets", [vp, u32, vp, vp, vp]),
+                 ("rle_dist_gather_offsets_async", [vp, u32, vp, vp, vp, vp, ctypes.c_int]),
                  ("rle_dist_offsets_device", [vp, u32, u32, vp, vp]),
                  ("rle_dist_finalize", [])):
         getattr(L, f).restype = ctypes.c_int
@@ -267,6 +273,21 @@ def gen_synthetic(d_out, off, length, kind=None, index=None, stream=None):
         raise RLEError(f"rle_gen_synthetic_device failed: {rc}")
 
 
+def copy_device(dst, src, nbytes, stream=None):
+    """rle_copy_device: the hand-written 16-byte-per-lane streaming copy bench.py times as the
+    practical HBM ceiling (not part of the codec).  nbytes must be a multiple of 16."""
+    rc = lib().rle_copy_device(_ptr(dst), _ptr(src), int(nbytes), _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_copy_device failed: {rc}")
+
+
+def set_coop_mode(mode: int):
+    """Tests: the cooperative small-buffer kernels never (0), always when the sizes qualify (1), or
+    when the launch is resident at once (-1, the default; RLE_MI355X_COOP sets it at load)."""
+    if lib().rle_mi355x_set_coop_mode(int(mode)) != RLE_OK:
+        raise RLEError(f"bad cooperative mode {mode}")
+
+
 def selftest() -> int:
     return int(lib().rle_mi355x_selftest())
 
@@ -302,6 +323,11 @@ def _torch_rccl_path():
     return p.encode() if os.path.exists(p) else None
 
 
+def dist_available():
+    """Raises unless RCCL resolves in this process (the preflight of shard.NativeExchange)."""
+    _check(lib().rle_dist_available(_torch_rccl_path()), "rle_dist_available")
+
+
 def dist_unique_id() -> bytes:
     buf = ctypes.create_string_buffer(128)
     _check(lib().rle_dist_unique_id(buf, 128, _torch_rccl_path()), "rle_dist_unique_id")
@@ -317,6 +343,14 @@ def dist_gather_offsets(sizes, gathered, offsets, stream=None):
     and scanned into offsets (int64[world * n]) in the global stream order."""
     _check(lib().rle_dist_gather_offsets(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets),
                                          _stream_ptr(stream)), "rle_dist_gather_offsets")
+
+
+def dist_gather_offsets_async(sizes, gathered, offsets, codec_stream, comm_stream, slot: int):
+    """The exchange on comm_stream after the work issued on codec_stream (rle_dist_gather_offsets_async);
+    codec_stream waits only for the previous call's exchange (the other slot)."""
+    _check(lib().rle_dist_gather_offsets_async(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets),
+                                               _stream_ptr(codec_stream), _stream_ptr(comm_stream), int(slot)),
+           "rle_dist_gather_offsets_async")
 
 
 def dist_offsets(gathered, world: int, n: int, offsets, stream=None):

@@ -45,16 +45,34 @@ class NativeExchange:
     torch calls on a side stream costs 56-87 us of host time per configs[1] step against ~21 us of
     GPU time (tools/exchange_cost.py).  Collective setup: every rank constructs it; rank 0's
     communicator id is broadcast over the process group.  `ok` is False on every rank unless every
-    rank's communicator came up (then callers use global_offsets)."""
+    rank's communicator came up (then callers use global_offsets).
+
+    Order of the collective setup, so that no rank can be left waiting in the blocking
+    communicator init for a rank that never enters it:
+      1. preflight: every rank resolves RCCL (rle_dist_available) and the flags are all-reduced
+         with MIN; if any rank failed, no rank goes further;
+      2. rank 0 creates the communicator id, broadcast over the process group;
+      3. every rank inits its communicator; the result flags are all-reduced with MIN again."""
 
     def __init__(self, n: int, world: int, rank: int, dev):
         import rle_mi355x as R
         self.R, self.n, self.world, self.ok = R, n, world, False
-        err = None
+        self.error = None
+        try:
+            R.dist_available()
+            avail = 1
+        except Exception as e:
+            avail, self.error = 0, e
+        t = torch.tensor([avail], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if not t.item():
+            if self.error is None:
+                self.error = RuntimeError("RCCL unavailable on another rank")
+            return
         try:
             uid = [R.dist_unique_id() if rank == 0 else None]
-        except Exception as e:   # no RCCL symbols: every rank learns it below
-            uid, err = [None], e
+        except Exception as e:   # every rank learns it from the broadcast
+            uid, self.error = [None], e
         dist.broadcast_object_list(uid, src=0)
         up = 0
         if uid[0] is not None:
@@ -62,23 +80,32 @@ class NativeExchange:
                 R.dist_init(uid[0], rank, world)
                 up = 1
             except Exception as e:
-                err = e
+                self.error = e
         t = torch.tensor([up], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         self.ok = bool(t.item())
-        self.error = err
         if not self.ok:
             if up:
                 R.dist_finalize()
             return
-        self.gathered = torch.empty(world * n, dtype=torch.int64, device=dev)
-        self.offsets = torch.empty(world * n, dtype=torch.int64, device=dev)
+        # two result buffers: the exchange of step i may still run (a graph branch) while step i + 1's
+        # is issued
+        self.gathered = [torch.empty(world * n, dtype=torch.int64, device=dev) for _ in range(2)]
+        self.offsets = [torch.empty(world * n, dtype=torch.int64, device=dev) for _ in range(2)]
 
-    def step(self, local_sizes: torch.Tensor, stream) -> torch.Tensor:
-        """Issue one exchange on `stream` after the work issued on it so far; returns the offsets
-        tensor (complete in stream order)."""
-        self.R.dist_gather_offsets(local_sizes, self.gathered, self.offsets, stream)
-        return self.offsets
+    def step(self, local_sizes: torch.Tensor, stream, slot: int = 0) -> torch.Tensor:
+        """Issue one exchange on `stream` after the work issued on it so far, into result buffer
+        `slot` (0 or 1); returns the offsets tensor (complete in stream order)."""
+        self.R.dist_gather_offsets(local_sizes, self.gathered[slot], self.offsets[slot], stream)
+        return self.offsets[slot]
+
+    def step_async(self, local_sizes: torch.Tensor, codec_stream, comm_stream, slot: int) -> torch.Tensor:
+        """The same exchange on comm_stream, ordered after the work issued on codec_stream so far;
+        codec_stream waits only for the previous call's exchange (rle_dist_gather_offsets_async).
+        Callers alternate slot 0 / 1 per step."""
+        self.R.dist_gather_offsets_async(local_sizes, self.gathered[slot], self.offsets[slot], codec_stream,
+                                         comm_stream, slot)
+        return self.offsets[slot]
 
     def close(self):
         if self.ok:

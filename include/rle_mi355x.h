@@ -68,11 +68,11 @@ int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const ui
 
 /* The same two launches with the batch's largest sizes known on the host (max_in_len >= every
  * d_in_len[i]; decode: max_out_len >= every d_out_len[i]).  Few small buffers (encode:
- * max_in_len <= 8 KiB; decode: max_in_len <= 8064 and max_out_len <= 16 KiB; and at most about
- * 6144 waves in all, one per tile) then run the cooperative kernels, one workgroup per buffer
- * and one wave per tile, so a buffer's tiles run side by side instead of one after another (a
- * single file, a small readN).  Other batches (or RLE_MI355X_COOP=0) take the kernels above.
- * Output and status are the same bytes. */
+ * max_in_len <= 8 KiB; decode: max_in_len <= 8064 and max_out_len <= 16 KiB; and no more
+ * workgroups than the chip holds at once, from the occupancy API) then run the cooperative
+ * kernels, one workgroup per buffer and one wave per tile, so a buffer's tiles run side by side
+ * instead of one after another (a single file, a small readN).  Other batches (or
+ * RLE_MI355X_COOP=0) take the kernels above.  Output and status are the same bytes. */
 int rle_encode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                   void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
                                   uint32_t* d_status, uint32_t n, uint64_t max_in_len, void* stream);
@@ -157,14 +157,35 @@ int rle_mi355x_timeline(unsigned long long* out, int reset);
  *   rle_dist_gather_offsets: on `stream`, after the work issued on it so far: all-gather
  *     d_sizes[n] into d_gathered[world * n] (rank major), then the exclusive scan in global order
  *     into d_offsets[world * n].
- *   rle_dist_offsets_device: the scan alone, on `stream` (tests).
+ *   rle_dist_offsets_device: the scan alone, on `stream` (tests).  Two launches over the whole
+ *     chip; the first call on a device allocates a small workspace, so make one before capturing
+ *     the exchange in a HIP graph.
+ *   rle_dist_available: RLE_OK when the RCCL symbols resolve in this process (a preflight that every
+ *     rank runs before any rank enters the blocking rle_dist_init).
  *   rle_dist_finalize: destroys the communicator. */
+int rle_dist_available(const char* rccl_path);
 int rle_dist_unique_id(void* out, size_t len, const char* rccl_path);
 int rle_dist_init(const void* id, size_t len, int rank, int world, const char* rccl_path);
 int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets,
                             void* stream);
 int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world, uint32_t n, int64_t* d_offsets, void* stream);
+/* rle_dist_gather_offsets off the codec's stream: after the work issued on codec_stream so far, the
+ * gather + scan run on comm_stream into the caller's result buffers of `slot` (0 or 1, alternating
+ * per step); codec_stream is made to wait only for the previous call's exchange (the other slot),
+ * so the caller may rewrite the other slot's sizes in its next step. */
+int rle_dist_gather_offsets_async(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets,
+                                  void* codec_stream, void* comm_stream, int slot);
 int rle_dist_finalize(void);
+
+/* Tests: the cooperative mode of the sized entry points, in-process (0 never, 1 whenever the sizes
+ * qualify, -1 residency-gated default; RLE_MI355X_COOP sets the initial mode).  RLE_E_INVAL
+ * otherwise. */
+int rle_mi355x_set_coop_mode(int mode);
+
+/* Measurement only (not the codec): copies nbytes (a multiple of 16, both pointers 16-byte aligned)
+ * from d_src to d_dst on `stream` with a hand-written 16-byte-per-lane streaming kernel; bench.py
+ * times it as the practical HBM ceiling of SURVEY.md §8(d).  RLE_E_INVAL on bad sizes. */
+int rle_copy_device(void* d_dst, const void* d_src, uint64_t nbytes, void* stream);
 
 /* Number of visible HIP devices (0 when none). */
 int rle_mi355x_device_count(void);

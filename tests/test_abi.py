@@ -132,3 +132,13 @@ def test_no_oracle_in_product_library():
     assert "oracle_" not in out
     ldd = subprocess.run(["ldd", R.LIB_PATH], capture_output=True, text=True).stdout
     assert "oracle" not in ldd and "librle_ref" not in ldd
+
+
+def test_fault_injection_only_in_test_build():
+    """The allocation-failure hook (RLE_MI355X_FAIL_ALLOC_ABOVE) is compiled into the test build
+    only: a leaked variable in a server's environment cannot make the product library fail."""
+    with open(R.LIB_PATH, "rb") as f:
+        assert b"RLE_MI355X_FAIL_ALLOC_ABOVE" not in f.read()
+    th = os.path.join(os.path.dirname(R.LIB_PATH), "build", "librle_mi355x_testhooks.so")
+    with open(th, "rb") as f:
+        assert b"RLE_MI355X_FAIL_ALLOC_ABOVE" in f.read()

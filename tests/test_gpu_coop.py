@@ -16,15 +16,11 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True, scope="module")
 def _always_coop():
     # the launcher's default takes the cooperative kernels only for launches resident at once;
-    # these tests run them for every batch (RLE_MI355X_COOP is read at each launch)
-    import os
-    old = os.environ.get("RLE_MI355X_COOP")
-    os.environ["RLE_MI355X_COOP"] = "1"
+    # these tests run them for every batch (the library's test setter, not the environment)
+    import rle_mi355x as R
+    R.set_coop_mode(1)
     yield
-    if old is None:
-        del os.environ["RLE_MI355X_COOP"]
-    else:
-        os.environ["RLE_MI355X_COOP"] = old
+    R.set_coop_mode(-1)
 
 
 def _hints(xs, ys):

@@ -17,7 +17,8 @@ def _ref_offsets(gathered, world, n):
     return np.cumsum(glob) - glob
 
 
-@pytest.mark.parametrize("world,n", [(1, 1), (2, 7), (3, 1000), (8, 4096), (8, 131072)])
+@pytest.mark.parametrize("world,n", [(1, 1), (2, 7), (3, 1000), (8, 4096), (8, 131072), (1, 1 << 20),
+                                     (5, 300000), (16, 65537), (17, 1000)])
 def test_offsets_kernel_global_order(world, n):
     rng = np.random.default_rng(world * 1000 + n)
     g = rng.integers(0, 70000, size=world * n, dtype=np.int64)
@@ -43,4 +44,85 @@ def test_exchange_step_one_rank():
         assert torch.equal(gathered, sizes)
         assert torch.equal(offsets, torch.cumsum(sizes, 0) - sizes)
     finally:
+        R.dist_finalize()
+
+
+def test_exchange_captured_in_graph_one_rank():
+    """The graph form bench.py uses at N > 1: the exchange issued on a branch stream inside a HIP
+    graph capture (fork / join by events), replayed several times, gives the same offsets."""
+    uid = R.dist_unique_id()
+    R.dist_init(uid, 0, 1)
+    try:
+        n = 4096
+        sizes = torch.randint(1, 6000, (n,), dtype=torch.int64, device=DEV)
+        gathered = torch.empty_like(sizes)
+        offsets = torch.full((n,), -1, dtype=torch.int64, device=DEV)
+        R.dist_gather_offsets(sizes, gathered, offsets)   # eager first: allocates the scan workspace
+        torch.cuda.synchronize()
+        offsets.fill_(-1)
+        g = torch.cuda.CUDAGraph()
+        main, side = torch.cuda.Stream(), torch.cuda.Stream()
+        main.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=main, capture_error_mode="relaxed"):
+            side.wait_stream(main)
+            R.dist_gather_offsets(sizes, gathered, offsets, side)
+            main.wait_stream(side)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            offsets.fill_(-1)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(offsets, torch.cumsum(sizes, 0) - sizes)
+        del g
+    finally:
+        R.dist_finalize()
+
+
+@pytest.mark.parametrize("xmode", ["async", "inline", "graph"])
+def test_bench_exchange_path_one_rank(xmode):
+    """bench.py's N > 1 rank loop rehearsed on one GPU (RLE_BENCH_FORCE_EXCHANGE=1): a one-rank
+    process group over RCCL, the native exchange in each mode (side stream, codec stream, captured
+    with the timed loop in one HIP graph), the offsets checked against the process-group path, and
+    the round trip verified."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RLE_BENCH_FORCE_EXCHANGE="1", RLE_BENCH_XMODE=xmode)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "6", "--warmup", "2", "--no-cpu",
+                        "--no-north-star", "--no-concurrent"], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["verified_bit_exact_roundtrip"] is True
+    assert out["exchange"]["mode"] == xmode, out["exchange"]
+    assert out["exchange"]["graph_captured"] is (True if xmode == "graph" else None)
+    assert out["exchange"]["offsets_match_process_group"] is True
+
+
+def test_exchange_async_alternating_slots():
+    """rle_dist_gather_offsets_async over several steps with the sizes rewritten every step (the
+    bench's pattern: slot i % 2): every step's offsets are that step's scan."""
+    uid = R.dist_unique_id()
+    R.dist_init(uid, 0, 1)
+    try:
+        n = 4096
+        codec, comm = torch.cuda.current_stream(), torch.cuda.Stream()
+        sizes = [torch.zeros(n, dtype=torch.int64, device=DEV) for _ in range(2)]
+        gathered = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(2)]
+        offsets = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(2)]
+        want = []
+        for i in range(6):
+            s = i % 2
+            v = torch.randint(1, 6000, (n,), dtype=torch.int64, device=DEV)
+            sizes[s].copy_(v)   # the "encode" of step i, on the codec stream
+            R.dist_gather_offsets_async(sizes[s], gathered[s], offsets[s], codec, comm, s)
+            want.append(torch.cumsum(v, 0) - v)
+            if i >= 4:
+                torch.cuda.synchronize()
+                assert torch.equal(offsets[s], want[i])
+    finally:
+        torch.cuda.synchronize()
         R.dist_finalize()

@@ -218,7 +218,10 @@ print("ok")
 '''
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
-    env = dict(os.environ, RLE_MI355X_FAIL_ALLOC_ABOVE=str(1 << 20))
+    # the hook is compiled only into the test build of the library (RLE_TEST_HOOKS)
+    testlib = os.path.join(root, "c-filestorage-server-and-client_amd", "build", "librle_mi355x_testhooks.so")
+    assert os.path.exists(testlib), "build() makes the test-hook library"
+    env = dict(os.environ, RLE_MI355X_FAIL_ALLOC_ABOVE=str(1 << 20), RLE_MI355X_LIB=testlib)
     r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "c-filestorage-server-and-client_amd"),
                         os.path.join(root, "oracle")], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout[-1000:], r.stderr[-2000:])

@@ -308,6 +308,49 @@ def test_full_size_shard_roundtrip_property():
         assert got == y, i
 
 
+def test_configs3_per_rank_shard_full_size():
+    """configs[3] at its real per-rank size: 1 M x 64 KiB sharded round-robin over 8 GPUs is 131072 x
+    64 KiB = 8 GiB per rank.  Rank 5's shard (global buffer i = 8 k + 5, data kind by local index as
+    bench.py's cfg3), generated on device from the global seeds; encode + decode in one launch each.
+    Checks: the device round trip is the identity over all 8 GiB, every status is clean, and every
+    global buffer i with i % 1021 == 0 in this shard is bit-exact against the
+    oracle, stream and size.  Buffers are independent (src/rleCompression.c:9-62 keeps no state
+    across calls), so one rank's shard is the whole per-GPU workload."""
+    world, rank, n, U = 8, 5, 131072, 65536
+    gidx = torch.arange(n, dtype=torch.int64, device=DEV) * world + rank
+    kinds = (torch.arange(n, dtype=torch.int32, device=DEV) % 4)
+    offs = torch.arange(n, dtype=torch.int64, device=DEV) * U
+    lens = torch.full((n,), U, dtype=torch.int64, device=DEV)
+    d_in = torch.empty(n * U, dtype=torch.uint8, device=DEV)
+    R.gen_synthetic(d_in, offs, lens, kinds, gidx)
+    cap = R.round16(R.max_compressed_size(U))
+    d_c = torch.empty(n * cap, dtype=torch.uint8, device=DEV)
+    coffs = torch.arange(n, dtype=torch.int64, device=DEV) * cap
+    clen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    est = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
+    R.encode_batch(d_in, offs, lens, d_c, coffs, clen, est)
+    d_out = torch.empty(n * U, dtype=torch.uint8, device=DEV)
+    st = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
+    R.decode_batch(d_c, coffs, clen, d_out, offs, lens, None, st)
+    torch.cuda.synchronize()
+    assert int(est.abs().sum().item()) == 0
+    assert int(st.abs().sum().item()) == 0
+    assert torch.equal(d_out, d_in)
+    del d_out
+    cl = clen.cpu().numpy()
+    sample = [k for k in range(n) if (k * world + rank) % 1021 == 0]
+    assert len(sample) >= 120
+    c_sum = 0
+    for k in sample:
+        x = O.gen(k % 4, k * world + rank, U)
+        assert d_in[k * U:(k + 1) * U].cpu().numpy().tobytes() == x, k
+        y = O.encode(x)
+        assert cl[k] == len(y), k
+        assert d_c[k * cap:k * cap + len(y)].cpu().numpy().tobytes() == y, k
+        c_sum += len(y)
+    assert c_sum == int(cl[sample].sum())
+
+
 @pytest.mark.parametrize("seg", [False, True])
 def test_decode_status_info_bits(seg):
     # encoder output is status 0, including streams that end in a single 0x00 token (the reference
