@@ -65,12 +65,13 @@ bool load_rccl(const char* path) {
 //                      of every rank into registers (world W a template constant up to 16), a
 //                      workgroup scan gives each k's offset, the W offsets of k go to LDS in global
 //                      order and leave as one coalesced run.
-// Small exchanges (n <= kSmallK, e.g. configs[1]'s 4096 sizes per rank) take one launch: a single
-// 512-thread workgroup walks the sub-tiles with a running carry, no workspace.  No division
-// anywhere.
-constexpr unsigned kScanThreads = 256, kSmallThreads = 512, kMaxTiles = 512;
+// Exchanges of at most kSmallK sizes per rank take one launch: a single 512-thread workgroup, one
+// sub-tile, no workspace.  (A single workgroup walking several sub-tiles in turn is slower than the
+// two launches: 17.4 us for 8 x 4096 against ~3-6 us per kernel, r3d rocprof.)  At 1 M entries the
+// two kernels take 10-12 us together (8 x 131072, r3d).  No division anywhere.
+constexpr unsigned kScanThreads = 256, kSmallThreads = 512, kMaxTiles = 2048;
 constexpr size_t kStageBytes = 32768;   // LDS staging of one sub-tile's outputs, at most
-constexpr uint32_t kSmallK = 8192;
+constexpr uint32_t kSmallK = kSmallThreads;
 
 template <unsigned T>
 __device__ __forceinline__ int64_t block_sum(int64_t v, int64_t* red) {

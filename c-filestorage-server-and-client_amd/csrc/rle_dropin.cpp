@@ -17,6 +17,7 @@
 // rle_fileops.h) are the fused and batched forms of the callers' compositions.
 #include <hip/hip_runtime.h>
 #include <pthread.h>
+#include <sched.h>
 #include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -27,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <new>
+#include <mutex>
 #include <vector>
 
 #include "rleCompression.h"
@@ -48,6 +50,7 @@ struct Stats {
     std::atomic<uint64_t> bytes_in{0}, bytes_out{0};        // caller bytes in / returned bytes out
     std::atomic<uint64_t> bytes_h2d{0}, bytes_d2h{0};
     std::atomic<uint64_t> ns_stage_in{0}, ns_device{0}, ns_stage_out{0};
+    std::atomic<uint64_t> calls_coalesced{0}, launches_coalesced{0};   // zero-copy calls / their combined launches
 } g_stats;
 inline uint64_t now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -98,6 +101,8 @@ constexpr int kPipeEvents = 16;
 // 19 / 20 us per compress / decompress call against 21 / 23 with one H2D + one D2H;
 // profiles/r1e_small.md).  RLE_MI355X_SMALL=copy selects the copying form.
 bool g_zerocopy = true;
+bool g_coalesce = false;   // concurrent zero-copy calls join one launch (submit); RLE_MI355X_COALESCE=1: on
+size_t g_presize = 1u << 20;   // staging allocated with each thread context (presize); RLE_MI355X_PRESIZE
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 
 // Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
@@ -135,6 +140,8 @@ struct Ctx {
     uint8_t* d_mid = nullptr; size_t d_mid_cap = 0;   // RLEappend: decoded old content ‖ new bytes
     uint8_t* h_bm = nullptr;  size_t h_bm_cap = 0;    // RLEdecompressN: per-file offsets/lengths/status
     uint8_t* d_bm = nullptr;  size_t d_bm_cap = 0;
+    uint8_t* h_cw = nullptr;                         // mapped launch words of combined launches (submit)
+    uint8_t* d_cw = nullptr;
 };
 // h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
 //   decode [in_off, in_len, out_off, out_len, out_cap, status], encode [in_off, in_len, out_off,
@@ -168,6 +175,7 @@ void free_ctx(void* p) {
     (void)hipHostFree(c->h_meta);
     (void)hipHostFree(c->h_bm);
     (void)hipHostFree(c->h_zc);
+    (void)hipHostFree(c->h_cw);
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_meta);
@@ -185,6 +193,8 @@ void init_once() {
     if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
+    if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RLE_MI355X_PRESIZE")) g_presize = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_STAGING")) {
         if (!strcmp(e, "pinned")) g_staging = Staging::Pinned;
         else if (!strcmp(e, "pipe")) g_staging = Staging::Pipe;
@@ -201,6 +211,8 @@ void init_once() {
 }
 
 inline size_t round16(size_t x) { return (x + 15u) & ~(size_t)15u; }
+
+void presize(Ctx* c);   // below
 
 Ctx* ctx() {
     pthread_once(&g_once, init_once);
@@ -226,6 +238,7 @@ Ctx* ctx() {
         throw std::bad_alloc();
     }
     pthread_setspecific(g_key, c);
+    presize(c);
     return c;
 }
 
@@ -434,17 +447,177 @@ uint8_t* zc(Ctx* c) {
     return c->h_zc;
 }
 
+// A new thread context gets its buffers at once: the zero-copy buffer and g_presize bytes of pinned
+// staging and device buffers each way, so that the first medium-size calls do not pay pinned-memory
+// growth (hipHostMalloc of a few hundred KiB costs milliseconds: r2i e2e, 7.6 ms of ns_stage_in for
+// 883 KB).  RLE_MI355X_PRESIZE=<bytes> (0: grow lazily).  A failed allocation here is not an error:
+// the buffers then grow on demand as before.
+void presize(Ctx* c) {
+    if (!g_presize) return;
+    try {
+        zc(c);
+        grow_host(c->h_in, c->h_in_cap, g_presize);
+        grow_host(c->h_out, c->h_out_cap, g_presize);
+        grow_dev(c->d_in, c->d_in_cap, g_presize);
+        grow_dev(c->d_out, c->d_out_cap, g_presize);
+    } catch (const std::bad_alloc&) {
+    }
+}
+
+// ---------------------------------------------------------------- coalescing of concurrent small calls
+// The server's worker threads (src/server.c:520-524) call the codec concurrently -- reads of
+// different files decode outside the store lock (src/filesystemApi.c:570 -> 597) -- and a 4 KiB
+// call is bound by its fixed cost (one launch, one sync: ~18 us), not by the GPU.  So concurrent
+// zero-copy calls on one device join one batched launch (flat combining): each caller puts its
+// bytes in its own mapped buffer and a request on the device's queue; whichever caller finds no
+// batch in flight becomes the combiner, takes every queued request, issues one encode and/or one
+// decode launch over all of them on its stream (the kernels read and write the callers' mapped
+// buffers; offsets are relative to the lowest buffer address), syncs once and marks each request
+// done.  Requests that arrive meanwhile wait for the next combiner.  A caller alone pays two mutex
+// operations more than before.  Outputs are the same bytes: each buffer is independent
+// (src/rleCompression.c:9-62).
+// Off by default (RLE_MI355X_COALESCE=1 turns it on): measured with tools/callrate (4 KiB round
+// trips, r3d), one stream per thread already overlaps the calls on the GPU's hardware queues --
+// 55.8 K calls/s on 1 thread, 98.7 K on 2, 250.6 K on 8, 291.7 K on 16 -- while combining serialises
+// them behind the batch in flight: 52.9 K, 145.2 K and 248.6 K calls/s on 2, 8 and 16 threads.
+constexpr uint32_t kMaxCoalesce = 256;   // requests per combined launch
+struct Req {
+    const uint8_t* d_buf;   // the caller's mapped buffer (device address): input at kZcIn, output at kZcOut
+    uint64_t in_len;        // encode: U; decode: C
+    uint64_t out_len;       // decode: U
+    uint64_t cap;           // decode: U + E
+    bool dec;
+    uint64_t result;        // encode: C; decode: status
+    std::atomic<int> done{0};
+};
+struct Combiner {
+    std::mutex m;
+    std::vector<Req*> q;
+    std::atomic<bool> busy{false};
+};
+constexpr int kMaxDev = 64;
+Combiner g_comb[kMaxDev];
+
+// Launch words of one combined launch in the combiner's mapped buffer: per kind 5 u64 arrays (in_off,
+// in_len, out_off, out_len, out_cap) and the u32 statuses.
+constexpr size_t kCwBytes = 2 * (5 + 1) * 8 * kMaxCoalesce;
+uint64_t* cw(Ctx* c, uint64_t** dev) {
+    if (!c->h_cw) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->h_cw), kCwBytes, hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            c->h_cw = nullptr;
+            throw std::bad_alloc();
+        }
+        check(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_cw), c->h_cw, 0), "hipHostGetDevicePointer");
+    }
+    *dev = reinterpret_cast<uint64_t*>(c->d_cw);
+    return reinterpret_cast<uint64_t*>(c->h_cw);
+}
+
+// One combined launch per kind over reqs[0, m), on c's stream, one sync.
+void run_batch(Ctx* c, Req* const* reqs, uint32_t m) {
+    uint64_t* dw = nullptr;
+    uint64_t* hw = cw(c, &dw);
+    const uint8_t* base = reqs[0]->d_buf;
+    for (uint32_t i = 1; i < m; ++i) base = std::min(base, reqs[i]->d_buf);
+    for (int dec = 0; dec < 2; ++dec) {
+        uint64_t* h = hw + (size_t)dec * (5 + 1) * kMaxCoalesce;   // 5 u64 arrays + room for the statuses
+        uint64_t* d = dw + (size_t)dec * (5 + 1) * kMaxCoalesce;
+        uint32_t k = 0;
+        uint64_t max_in = 0, max_out = 0;
+        for (uint32_t i = 0; i < m; ++i) {
+            const Req* r = reqs[i];
+            if (r->dec != (dec != 0)) continue;
+            const uint64_t off = (uint64_t)(r->d_buf - base);
+            h[k] = off + kZcIn;
+            h[kMaxCoalesce + k] = r->in_len;
+            h[2 * kMaxCoalesce + k] = off + kZcOut;
+            h[3 * kMaxCoalesce + k] = r->out_len;
+            h[4 * kMaxCoalesce + k] = r->cap;
+            max_in = std::max(max_in, r->in_len);
+            max_out = std::max(max_out, r->out_len);
+            ++k;
+        }
+        if (!k) continue;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(d + 5 * kMaxCoalesce);
+        uint8_t* obase = const_cast<uint8_t*>(base);
+        const int rc = dec ? rle_decode_batch_device_sized(base, d, d + kMaxCoalesce, obase, d + 2 * kMaxCoalesce,
+                                                           d + 3 * kMaxCoalesce, d + 4 * kMaxCoalesce, dst, k, max_in,
+                                                           max_out, c->s)
+                           : rle_encode_batch_device_sized(base, d, d + kMaxCoalesce, obase, d + 2 * kMaxCoalesce,
+                                                           d + 3 * kMaxCoalesce, dst, k, max_in, c->s);
+        if (rc != RLE_OK) die(dec ? "decode launch" : "encode launch", hipGetLastError());
+    }
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    uint32_t ke = 0, kd = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        Req* r = reqs[i];
+        if (r->dec) {
+            const uint32_t* st = reinterpret_cast<const uint32_t*>(hw + (5 + 1) * kMaxCoalesce + 5 * kMaxCoalesce);
+            r->result = st[kd++];
+        } else {
+            r->result = hw[3 * kMaxCoalesce + ke++];
+        }
+        r->done.store(1, std::memory_order_release);
+    }
+    g_stats.launches_coalesced++;
+    g_stats.calls_coalesced += m;
+}
+
+// Queue r on the device's combiner and return once it is done (this thread may run the batch).
+void submit(Ctx* c, Req* r) {
+    Combiner& cb = g_comb[c->dev % kMaxDev];
+    {
+        std::lock_guard<std::mutex> g(cb.m);
+        cb.q.push_back(r);
+    }
+    Req* batch[kMaxCoalesce];
+    for (unsigned spin = 0; !r->done.load(std::memory_order_acquire); ++spin) {
+        if (!cb.busy.load(std::memory_order_relaxed) && !cb.busy.exchange(true, std::memory_order_acquire)) {
+            uint32_t m = 0;
+            {
+                std::lock_guard<std::mutex> g(cb.m);
+                m = (uint32_t)std::min<size_t>(cb.q.size(), kMaxCoalesce);
+                std::copy(cb.q.begin(), cb.q.begin() + m, batch);
+                cb.q.erase(cb.q.begin(), cb.q.begin() + m);
+            }
+            if (m) {
+                try {
+                    run_batch(c, batch, m);
+                } catch (...) {   // allocation failure of the launch words: every waiter must still finish
+                    for (uint32_t i = 0; i < m; ++i) {
+                        batch[i]->result = ~0ull;
+                        batch[i]->done.store(1, std::memory_order_release);
+                    }
+                }
+            }
+            cb.busy.store(false, std::memory_order_release);
+        } else if (spin > 64) {
+            sched_yield();
+        }
+    }
+    if (r->result == ~0ull) throw std::bad_alloc();
+}
+
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, U);
-    uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
-    hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0;
-    uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-    if (rle_encode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
-                                      reinterpret_cast<uint32_t*>(dw + 4), 1, U, c->s) != RLE_OK)
-        die("encode launch", hipGetLastError());
-    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-    const size_t C = hw[3];
+    size_t C;
+    if (g_coalesce) {
+        Req r;
+        r.d_buf = c->d_zc; r.in_len = U; r.out_len = 0; r.cap = 0; r.dec = false; r.result = 0;
+        submit(c, &r);
+        C = r.result;
+    } else {
+        uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
+        hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0;
+        uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+        if (rle_encode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
+                                          reinterpret_cast<uint32_t*>(dw + 4), 1, U, c->s) != RLE_OK)
+            die("encode launch", hipGetLastError());
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        C = hw[3];
+    }
     *compressedSize = C;
     char* r = static_cast<char*>(malloc(C + 16));
     if (!r) return nullptr;
@@ -457,14 +630,22 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
     const size_t total = U + E;
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, C);
-    uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
-    hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
-    uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-    if (rle_decode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
-                                      reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, c->s) != RLE_OK)
-        die("decode launch", hipGetLastError());
-    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-    const uint32_t st = (uint32_t)hw[5];
+    uint32_t st;
+    if (g_coalesce) {
+        Req r;
+        r.d_buf = c->d_zc; r.in_len = C; r.out_len = U; r.cap = total; r.dec = true; r.result = 0;
+        submit(c, &r);
+        st = (uint32_t)r.result;
+    } else {
+        uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
+        hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
+        uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+        if (rle_decode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
+                                          reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, c->s) != RLE_OK)
+            die("decode launch", hipGetLastError());
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        st = (uint32_t)hw[5];
+    }
     memcpy(r, h + kZcOut, U);
     if (E) {
         if (st & RLE_STATUS_SERIAL) memcpy(r + U, h + kZcOut + U, E);
@@ -999,10 +1180,14 @@ extern "C" int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset) {
     out->ns_stage_in = g_stats.ns_stage_in.load();
     out->ns_device = g_stats.ns_device.load();
     out->ns_stage_out = g_stats.ns_stage_out.load();
+    out->calls_coalesced = g_stats.calls_coalesced.load();
+    out->launches_coalesced = g_stats.launches_coalesced.load();
     if (reset) {
         g_stats.calls_compress = 0; g_stats.calls_decompress = 0; g_stats.calls_append = 0; g_stats.bytes_in = 0; g_stats.bytes_out = 0;
         g_stats.bytes_h2d = 0; g_stats.bytes_d2h = 0; g_stats.ns_stage_in = 0; g_stats.ns_device = 0;
         g_stats.ns_stage_out = 0;
+        g_stats.calls_coalesced = 0;
+        g_stats.launches_coalesced = 0;
     }
     return RLE_OK;
 }
@@ -1021,12 +1206,13 @@ struct StatsAtExit {
         fprintf(f,
                 "{\"calls_compress\": %llu, \"calls_decompress\": %llu, \"calls_append\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, "
                 "\"bytes_h2d\": %llu, \"bytes_d2h\": %llu, \"ns_stage_in\": %llu, \"ns_device\": %llu, "
-                "\"ns_stage_out\": %llu}\n",
+                "\"ns_stage_out\": %llu, \"calls_coalesced\": %llu, \"launches_coalesced\": %llu}\n",
                 (unsigned long long)s.calls_compress, (unsigned long long)s.calls_decompress,
                 (unsigned long long)s.calls_append,
                 (unsigned long long)s.bytes_in, (unsigned long long)s.bytes_out, (unsigned long long)s.bytes_h2d,
                 (unsigned long long)s.bytes_d2h, (unsigned long long)s.ns_stage_in, (unsigned long long)s.ns_device,
-                (unsigned long long)s.ns_stage_out);
+                (unsigned long long)s.ns_stage_out, (unsigned long long)s.calls_coalesced,
+                (unsigned long long)s.launches_coalesced);
         fclose(f);
     }
 } g_stats_at_exit;

@@ -96,6 +96,8 @@ typedef struct {
     uint64_t bytes_in, bytes_out, bytes_h2d, bytes_d2h;
     uint64_t ns_stage_in, ns_device, ns_stage_out;
     uint64_t calls_append;   /* RLEappend (include/rle_fileops.h); RLEdecompressN counts per file */
+    uint64_t calls_coalesced, launches_coalesced;   /* zero-copy small calls and the combined launches
+                                                       they ran in (concurrent callers share one) */
 } rle_dropin_stats_t;
 int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
 

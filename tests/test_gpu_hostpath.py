@@ -1,0 +1,142 @@
+"""GPU tests of the drop-in's host path (BASELINE configs[4]).
+
+* Every staging mode of the large-call transfers (RLE_MI355X_STAGING = direct / pinned / pipe, read
+  at library init: a fresh process each) gives the oracle's bytes for RLEcompress / RLEdecompress
+  across the size thresholds (zero-copy small calls, pinned one-trip, segmented, >= 256 KiB
+  pipelined), for RLEappend and for RLEdecompressN with a file past the staging cap.
+* Concurrent small calls from many threads (the server's worker pool, src/server.c:520-524) stay
+  bit-exact, on per-thread streams (the default) and combined into shared launches
+  (RLE_MI355X_COALESCE=1): each thread's streams against the oracle, and the C call-rate tool's
+  round trips.
+"""
+import json
+import os
+import subprocess
+import sys
+import threading
+
+import pytest
+
+import rle_mi355x as R
+import rle_oracle as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+_STAGING_CODE = r'''
+import sys
+sys.path[:0] = sys.argv[1:3]
+import rle_mi355x as R, rle_oracle as O
+sizes = [1, 13, 4096, 40000, 70000, 200000, 300000, 2 << 20, 5 << 20]
+for i, U in enumerate(sizes):
+    for kind in (0, 1, 2, 3):
+        x = O.gen(kind, 1000 * i + kind, U)
+        y = O.encode(x)
+        assert R.compress(x) == y, (U, kind)
+        assert R.decompress(y, U) == x, (U, kind)
+        assert R.decompress(y, U, 777) == x + bytes(777), (U, kind)
+# the write path (src/filesystemApi.c:766-775) fused
+for U, A in ((4096, 4096), (300000, 70000), (3 << 20, 1 << 20)):
+    old = O.gen(2, U, U)
+    new = O.gen(3, A, A)
+    assert R.append(O.encode(old), U, new) == O.encode(old + new), (U, A)
+# readNFiles: small files, one past the 64 KiB staging cap set below, an empty one
+xs = [O.gen(k % 4, 50 + k, s) for k, s in enumerate([4096, 300000, 1000, 0, 70000, 2 << 20])]
+assert R.decompress_n([O.encode(x) for x in xs], [len(x) for x in xs]) == xs
+print("ok", R.dropin_stats())
+'''
+
+
+@pytest.mark.parametrize("mode", ["direct", "pinned", "pipe"])
+def test_staging_modes_bit_exact(mode):
+    env = dict(os.environ, RLE_MI355X_STAGING=mode, RLE_MI355X_STAGE_CAP=str(1 << 20))
+    r = subprocess.run([sys.executable, "-c", _STAGING_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
+                        os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+
+
+_COALESCE_CODE = r'''
+import sys, threading
+sys.path[:0] = sys.argv[1:3]
+import rle_mi355x as R, rle_oracle as O
+R.dropin_stats(reset=True)
+errors = []
+inputs = [[O.gen(k % 4, 7000 + 100 * t + k, 4096 + 9000 * (k % 5)) for k in range(40)] for t in range(16)]
+refs = [[O.encode(x) for x in xs] for xs in inputs]
+
+def work(t):
+    try:
+        for x, y in zip(inputs[t], refs[t]):
+            if R.compress(x) != y:
+                errors.append(("enc", t, len(x)))
+            if R.decompress(y, len(x), 3) != x + bytes(3):
+                errors.append(("dec", t, len(x)))
+    except Exception as e:   # surfaced below
+        errors.append(repr(e))
+
+th = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+assert not errors, errors[:5]
+st = R.dropin_stats()
+# every compress is a zero-copy call (U < 48 KiB); decompress is from C < 32 KiB
+small = 16 * 40 + sum(len(y) < (32 << 10) for ys in refs for y in ys)
+assert st["calls_coalesced"] == small
+assert 0 < st["launches_coalesced"] <= st["calls_coalesced"]
+print("ok", st)
+'''
+
+
+def test_concurrent_small_calls_coalesced_bit_exact():
+    """With call coalescing on (RLE_MI355X_COALESCE=1, read at init: a fresh process): 16 Python
+    threads, each 40 round trips of its own 4 KiB - 40 KiB buffers through the drop-in, every stream
+    against the oracle; the library counts every small call as combined."""
+    env = dict(os.environ, RLE_MI355X_COALESCE="1")
+    r = subprocess.run([sys.executable, "-c", _COALESCE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
+                        os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+
+
+def test_concurrent_small_calls_per_thread_streams_bit_exact():
+    """The default (one stream per calling thread, no combining): 16 threads of 4 KiB - 40 KiB round
+    trips against the oracle, and no call was combined."""
+    R.dropin_stats(reset=True)
+    errors = []
+    inputs = [[O.gen(k % 4, 9000 + 100 * t + k, 4096 + 9000 * (k % 5)) for k in range(20)] for t in range(16)]
+
+    def work(t):
+        try:
+            for x in inputs[t]:
+                y = O.encode(x)
+                if R.compress(x) != y or R.decompress(y, len(x)) != x:
+                    errors.append((t, len(x)))
+        except Exception as e:
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+    assert R.dropin_stats()["calls_coalesced"] == 0
+
+
+@pytest.mark.parametrize("coalesce", ["0", "1"])
+def test_callrate_tool_round_trips(coalesce):
+    """The C call-rate tool (8 threads x 4 KiB, 1 s): every round trip exact, with and without
+    call coalescing; with it, fewer launches than calls."""
+    exe = os.path.join(ROOT, "tools", "callrate")
+    assert os.path.exists(exe), "build() compiles tools/callrate"
+    r = subprocess.run([exe, "8", "4096", "1"], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, RLE_MI355X_COALESCE=coalesce))
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["bad"] == 0 and out["calls"] > 0
+    if coalesce == "1":
+        assert out["launches_coalesced"] < out["calls_coalesced"]
+    else:
+        assert out["calls_coalesced"] == 0
