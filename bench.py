@@ -94,6 +94,10 @@ WORKLOADS = {
     "s4k_mix": dict(n=65536, size=4096, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3", desc="65536 x 4 KiB zero/random/runs50/runs90"),
     "one4m": dict(n=1, size=4 << 20, kinds=(1,), ref_kinds="1", desc="1 x 4 MiB random (one large file)"),
     "one64m": dict(n=1, size=64 << 20, kinds=(2,), ref_kinds="2", desc="1 x 64 MiB runs50 (one large file)"),
+    # configs[2]'s 1 MiB end (the sweep's last rows; segmented-path A/B)
+    "m1_zero": dict(n=1024, size=1 << 20, kinds=(0,), ref_kinds="0", desc="1024 x 1 MiB zero"),
+    "m1_random": dict(n=1024, size=1 << 20, kinds=(1,), ref_kinds="1", desc="1024 x 1 MiB random"),
+    "m1_runs50": dict(n=1024, size=1 << 20, kinds=(2,), ref_kinds="2", desc="1024 x 1 MiB runs50"),
     "mixed": dict(n=1024, size=None, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",
                   desc="configs[2]: 1024 mixed 4 KiB-1 MiB buffers per GPU (zero / random / runs50 / runs90)"),
     "cfg3": dict(n=131072, size=65536, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3",

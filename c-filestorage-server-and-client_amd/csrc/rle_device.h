@@ -261,6 +261,22 @@ __device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
     // Loads are all consumed by the last step, so only a walk that stops early (~0u) drains.
     if (!primed) walk_prime<kStep, kLook>(rs, start, ntiles, lane, slots);
     u32 p1 = 0, p2 = 0;   // stores of the last step and of the one before
+#ifndef RLE_WALK_ROLLED   // 1: one copy of the step (slot chosen per tile) instead of two (code size)
+#define RLE_WALK_ROLLED 0
+#endif
+    if (RLE_WALK_ROLLED) {
+        for (u32 t = 0; t < ntiles; ++t) {
+            const u32 odd = t & 1u;
+            vm_wait(p2 + (t + 1u < ntiles ? kLoads : 0u) + p1);
+            p2 = p1;
+            p1 = step(t, slots + odd * kStride, Refill{rs, (t + 2u) * kStep + lo, odd ? l1 : l0, t + 2u < ntiles, look});
+            if (p1 == ~0u) {
+                vm_drain();
+                return true;
+            }
+        }
+        return false;
+    }
     for (u32 t = 0; t < ntiles; t += 2) {
         vm_wait(p2 + (t + 1u < ntiles ? kLoads : 0u) + p1);
         p2 = p1;
@@ -1416,7 +1432,10 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
     const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
-    if (kFast && RLE_DEC_FAST && !st.head) {
+    // In a segment (Co < C) the literal path takes no tail tile: its tail form masks at the stream's
+    // end, not at the segment's, and its last store may reach past the tile's output, which only a
+    // later tile of the same wave rewrites (a segment's last tile is always a tail tile).
+    if (kFast && RLE_DEC_FAST && !st.head && (!pr.tail || Co == C)) {
         const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
                               : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
         if (r != kNotFast) return r;

@@ -31,6 +31,9 @@ constexpr u32 kNone = 0xFFFFFFFFu;
 // per-buffer flags (workspace) written by the scans, read by the writers
 constexpr u32 kFlagSkip = 1u;     // bad buffer: status already written
 constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the whole buffer
+#ifndef RLE_SEG_FAST   // the write passes take the fast tile paths (round 3); 0: general path only
+#define RLE_SEG_FAST 1
+#endif
 
 // Segments of an n-byte buffer: n = q S + r gives q + (r >= 3) segments (at least one); the last
 // absorbs a remainder of 1-2 bytes, so a stream's final token never starts a segment of its own.
@@ -219,10 +222,13 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
                                                                   const u32* __restrict__ bflag) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kEncStage];
+    __shared__ __attribute__((aligned(16))) u32 elut[kInsWaveWords];   // enc_tile_fast's selectors
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     uint8_t* stage = stage_all + wid * kEncStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    for (u32 k = threadIdx.x; k < kInsWaveWords; k += kSegBlock) elut[k] = kEncInsLut.s[k];
+    __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
     for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
@@ -241,7 +247,9 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, false, {}};
         const EncK kc = enc_k();
         walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return enc_tile<false>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc);
+            // the fast tile paths (round 3; until then only the one-wave kernels took them): past the
+            // segment's shared first chunk and before its last tile, as in a one-wave walk
+            return enc_tile<false, RLE_SEG_FAST>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc, elut);
         });
         // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past this
         // segment's output and nothing before it
@@ -378,9 +386,13 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kDecStage];
     __shared__ DecEntry tbl[256];
+    __shared__ u32x4 clut[kCompactEntries];   // dec_tile_fast's selectors
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     for (u32 k = threadIdx.x; k < 256u; k += kSegBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
+    for (u32 k = threadIdx.x; k < kCompactEntries; k += kSegBlock)
+        clut[k] = u32x4{kCompactLut.s[4u * k], kCompactLut.s[4u * k + 1u], kCompactLut.s[4u * k + 2u],
+                        kCompactLut.s[4u * k + 3u]};
     uint8_t* stage = stage_all + wid * kDecStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
     for (u32 k = lane; k < kDecStage / 16u; k += kWave)
@@ -413,7 +425,9 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, false, {}};
         const DecK kc = dec_k();
         const bool serial = walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            return dec_tile(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc);
+            // the fast tile paths (round 3): past the segment's shared first chunk, and the literal
+            // path only on tiles a later tile of this segment follows (dec_tile)
+            return dec_tile<RLE_SEG_FAST>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc, clut);
         });
         const bool last = g + 1u == s0 + nseg;
         dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);

@@ -257,3 +257,45 @@ def test_literal_last_tiles_encode_match_oracle():
                     y[-3] ^= 0x5A
                 xs.append(bytes(y))
     _oracle_parity(xs)
+
+
+def test_periodic_tiles_decode_match_oracle():
+    """Periodic streams ("v v 9" tokens of one byte v: v = 0x00, '9', '0', random), which the
+    single-value tiles decode (dec_tile_fill), entered at every phase (a 1- or 3-byte token first),
+    and the same streams with the pattern broken once -- another count digit, another byte at a
+    token start, a literal, a stray byte -- at positions all over a tile and at its edges, so that
+    the general path decodes those tiles; also U short of / past the decoded length.  (Round 3 also
+    tried a dedicated periodic-tile path ahead of the phase scan: slower)"""
+    rng = np.random.default_rng(33)
+    ys = []
+    for v in (0x00, 0x39, 0x30, 0x61, int(rng.integers(0, 256))):
+        tok = bytes([v, v, 0x39])
+        for lead in (b"", b"\x01", b"\x02\x02\x35", b"\x07", b"\x03\x03\x32\x04"):
+            base = lead + tok * 1400   # ~4 tiles of tokens
+            ys.append(base)
+            for p in (len(lead), len(lead) + 1, len(lead) + 2, 500, 1006, 1007, 1008, 1009, 1010, 1500,
+                      2015, 2016, 2017, 3023, 3024, 3025, len(base) - 5):
+                for b in (0x38, v ^ 0x40, 0x31, 0x00):
+                    y = bytearray(base)
+                    y[p] = b
+                    ys.append(bytes(y))
+                y = bytearray(base)   # a literal inserted
+                ys.append(bytes(y[:p]) + bytes([v ^ 0x55]) + bytes(y[p:]))
+    def size(s):   # the decoded length with counts clamped to 1..9 (the oracle decides the rest)
+        U, j = 0, 0
+        while j < len(s):
+            if j + 1 < len(s) and s[j] == s[j + 1]:
+                U += min(9, max(1, s[j + 2] - 48)) if j + 2 < len(s) else 1
+                j += 3
+            else:
+                U += 1
+                j += 1
+        return U
+
+    us = [size(y) for y in ys]
+    for delta in (0, -7, 4):
+        uu = [max(0, u + delta) for u in us]
+        dec, st = gpu_decode(ys, uu)
+        for i, y in enumerate(ys):
+            ref, _ = O.decode(y, uu[i])
+            assert dec[i] == ref, (delta, i)
