@@ -1290,30 +1290,53 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     const u32 sa = __builtin_amdgcn_perm(0u, pr.ta.x, 0x0C0C0C00u | dl);
     const u32 sb = __builtin_amdgcn_perm(0u, pr.tb.x, 0x0C0C0C00u | mid);
     const u32 P16 = (sa | (sb << 8)) & ~NE16 & lim;   // pair starts (bits 0..15)
-    // every pair's count digit (position j + 2) is '2' (and, in a tail tile, lies below C)
-    const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
-                       alignbyte(pr.la, w[3], 2)};
-    u32 nz[4];
-#pragma unroll
-    for (u32 k = 0; k < 4; ++k) {
-        const u32 t = dg[k] ^ 0x32323232u;
-        nz[k] = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80);
-    }
-    const u32 za = __builtin_amdgcn_udot4(nz[1], kc.C2, __builtin_amdgcn_udot4(nz[0], kc.C1, 0u, false), false);
-    const u32 zb = __builtin_amdgcn_udot4(nz[3], kc.C2, __builtin_amdgcn_udot4(nz[2], kc.C1, 0u, false), false);
-    u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
-    if (kTail) NZ16 |= ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2);   // ... or lies past C
+#ifndef RLE_DEC_DIGIT2   // 1: the '2' test reads only the deleted digit bytes (round 3); 0: every position's digit
+#define RLE_DEC_DIGIT2 1
+#endif
     // deleted positions: digits of pairs started in this lane or (bits 14, 15) the lane before, and
     // in lane 0 the tile's first d positions; lane 63 keeps only a pair's second byte at position 0
     const u32 prevP = from_prev_lane(P16, 0u);
-    u32 del = ((P16 << 2) | (prevP >> 14)) & lim;
-    if (lane == 0u) del |= lowmask(st.d) & lim;
+    const u32 dig = ((P16 << 2) | (prevP >> 14)) & lim;   // the digits
+    const u32 del = lane == 0u ? dig | (lowmask(st.d) & lim) : dig;
+    bool reject;
+    if (RLE_DEC_DIGIT2) {
+        // every pair's count digit is '2': the digits are exactly the deleted positions other than
+        // lane 0's first d (the previous tile's token, checked there) -- on lane 63 only those of
+        // lane 62's pairs.  At most 2 per lane pass the limit below, so only those bytes are read
+        // (one v_perm pair each), not a '2' test of every position.
+        const u32 chk = lane < kOwnLanes ? dig : ((prevP >> 14) & 3u);
+        const u32 c1 = (u32)__builtin_ctz(chk | 0x10000u), c2 = (u32)__builtin_ctz((chk & (chk - 1u)) | 0x10000u);
+        auto byte_at = [&](u32 q) {   // byte q (0..15) of the lane's 16 bytes, in bits 0..7
+            const u32 lo = __builtin_amdgcn_perm(w[1], w[0], q & 7u), hi = __builtin_amdgcn_perm(w[3], w[2], q & 7u);
+            return (q & 8u) ? hi : lo;
+        };
+        const bool bad1 = c1 < 16u && (byte_at(c1) & 0xFFu) != 0x32u;
+        const bool bad2 = c2 < 16u && (byte_at(c2) & 0xFFu) != 0x32u;
+        // (lane 63's own pairs belong to the next tile: only its digit test counts, so the ballot
+        // below takes every lane)
+        reject = bad1 || bad2 || (lane < kOwnLanes && __builtin_popcount(del) > 2);
+        if (kTail) reject = reject || (lane < kOwnLanes && (P16 & ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2)) != 0u);
+    } else {
+        // every pair's count digit (position j + 2) is '2' (and, in a tail tile, lies below C)
+        const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
+                           alignbyte(pr.la, w[3], 2)};
+        u32 nz[4];
+#pragma unroll
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 t = dg[k] ^ 0x32323232u;
+            nz[k] = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80);
+        }
+        const u32 za = __builtin_amdgcn_udot4(nz[1], kc.C2, __builtin_amdgcn_udot4(nz[0], kc.C1, 0u, false), false);
+        const u32 zb = __builtin_amdgcn_udot4(nz[3], kc.C2, __builtin_amdgcn_udot4(nz[2], kc.C1, 0u, false), false);
+        u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
+        if (kTail) NZ16 |= ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2);   // ... or lies past C
+        reject = (P16 & NZ16) != 0u || __builtin_popcount(del) > 2;
+    }
     const u32 K = lane < kOwnLanes ? (~del & lim) : ((prevP >> 15) & 1u);
     const u32 kept = (u32)__builtin_popcount(K);
-    const bool reject = (P16 & NZ16) != 0u || __builtin_popcount(del) > 2;
     const u32 oincl = wave_scan_incl(kept, 0u, OpAdd());
     const u32 ttot = readlane(oincl, kWave - 1u);
-    if (__builtin_amdgcn_ballot_w64(reject) & kOwned) return kNotFast;
+    if (__builtin_amdgcn_ballot_w64(reject) & (RLE_DEC_DIGIT2 ? ~0ull : kOwned)) return kNotFast;
     if (kTail ? (ttot < 4u || st.out_pos + ttot > U) : st.out_pos + ttot + 16u > U) return kNotFast;
 
     u32 rounds = 0;

@@ -640,7 +640,10 @@ extern "C" int rle_copy_device(void* d_dst, const void* d_src, uint64_t nbytes, 
     const uint64_t n16 = nbytes / 16u;
     const uint64_t want = (n16 + 1023u) / 1024u;
     const uint32_t grid = (uint32_t)(want < 2048u ? want : 2048u);   // 8 workgroups per CU at most
-    static const bool nt = getenv("RLE_MI355X_COPY_NT") && !strcmp(getenv("RLE_MI355X_COPY_NT"), "1");
+    // non-temporal past the Infinity Cache's 256 MiB (dec64k's 1.82 GB: 311.6 against 331.8 us), plain
+    // below it (configs[1]'s 28 MB: 4.7 against 5.5 us); RLE_MI355X_COPY_NT=0/1 forces either
+    static const int force = getenv("RLE_MI355X_COPY_NT") ? atoi(getenv("RLE_MI355X_COPY_NT")) : -1;
+    const bool nt = force >= 0 ? force != 0 : nbytes >= (256ull << 20);
     if (nt)
         hipLaunchKernelGGL(rle::copy_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (rle::u32x4*)d_dst,
                            (const rle::u32x4*)d_src, n16);

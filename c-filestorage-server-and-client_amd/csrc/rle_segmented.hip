@@ -34,6 +34,9 @@ constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the w
 #ifndef RLE_SEG_FAST   // the write passes take the fast tile paths (round 3); 0: general path only
 #define RLE_SEG_FAST 1
 #endif
+#ifndef RLE_SEG_SUMFAST   // the summaries count uniform / literal tiles without the full analysis (round 3)
+#define RLE_SEG_SUMFAST 1
+#endif
 
 // Segments of an n-byte buffer: n = q S + r gives q + (r >= 3) segments (at least one); the last
 // absorbs a remainder of 1-2 bytes, so a stream's final token never starts a segment of its own.
@@ -131,7 +134,31 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_
             walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
                 nx();
-                const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, p0 + t * kTileStep, U, p1, lane, prev_top, rs, kc);
+                const u32 pos = p0 + t * kTileStep;
+                // (tried only when the run entering the tile is already 16 bytes long, a scalar test
+                // that keeps the check off random and short-run tiles)
+                if (RLE_SEG_SUMFAST && pos != 0u && pos - rs >= 16u && pos + kTileStep < p1) {
+                    // a tile inside a run (every byte, and the first lookahead byte, equal to the byte
+                    // before the tile; never the buffer's first tile, whose position 0 is a boundary
+                    // whatever its byte): no boundary, so fb, lb and rs stay; the tokens count only past
+                    // the segment's first boundary, all 3-byte (the run goes on), one every 9 bytes
+                    // from the run start rs.  About 10 VALU against enc_analyze's ~75.
+                    const u32 v = uniform(readlane(cur.x, 0)) & 0xFFu;
+                    if ((prev_top >> 24) == v) {
+                        const u32 vrep = v * 0x01010101u;
+                        const bool diff = lane < kOwnLanes
+                                              ? ((cur.x ^ vrep) | (cur.y ^ vrep) | (cur.z ^ vrep) | (cur.w ^ vrep)) != 0u
+                                              : ((cur.x ^ vrep) & 0xFFu) != 0u;
+                        if (!__builtin_amdgcn_ballot_w64(diff)) {
+                            if (fb != kNone) {
+                                const u32 f = pos + (9u - (pos - rs) % 9u) % 9u;   // first token start
+                                if (f < pos + kTileStep) rest += 3u * ((pos + kTileStep - 1u - f) / 9u + 1u);
+                            }
+                            return 0u;
+                        }
+                    }
+                }
+                const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, pos, U, p1, lane, prev_top, rs, kc);
                 // run boundaries inside the segment: the first one (L0) and the last one (lb)
                 const u32 Bo = an.B & an.validm;
                 const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
@@ -259,6 +286,42 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
 }
 
 // ================================================================ DECODE
+// Decoded bytes of a non-tail tile entered at phase d when every pair token in it is "v v 2" (random
+// and text-like data): then each token's output is its own bytes with the count digit deleted, so
+// the count is the owned positions minus the pairs' digits minus the tile's first d positions (the
+// literal path's count, dec_tile_fast, without its stores or its per-lane limits).  kNotFast when a
+// pair has another count (the caller then runs dec_lengths).  About 40 VALU against ~100 for
+// dec_lengths + its sum.
+__device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 lane, const DecK& kc) {
+    constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+    const u32* w = pr.w;
+    const u32 NE16 = (pr.xa >> 7) | (pr.xb << 1);
+    // cheap reject first (runs): at most 2 equal neighbours per owned lane
+    if (__builtin_amdgcn_ballot_w64(__builtin_popcount(~NE16 & 0xFFFFu) > 2) & kOwned) return kNotFast;
+    const u32 dl = bfe(pr.excl, 8u * d, 8);
+    const u32 mid = __builtin_amdgcn_perm(0u, pr.ta.y, 0x0C0C0C00u | dl);
+    const u32 sa = __builtin_amdgcn_perm(0u, pr.ta.x, 0x0C0C0C00u | dl);
+    const u32 sb = __builtin_amdgcn_perm(0u, pr.tb.x, 0x0C0C0C00u | mid);
+    const u32 P16 = (sa | (sb << 8)) & ~NE16 & 0xFFFFu;   // pair starts
+    const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
+                       alignbyte(pr.la, w[3], 2)};
+    u32 nz[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 t = dg[k] ^ 0x32323232u;
+        nz[k] = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80);
+    }
+    const u32 za = __builtin_amdgcn_udot4(nz[1], kc.C2, __builtin_amdgcn_udot4(nz[0], kc.C1, 0u, false), false);
+    const u32 zb = __builtin_amdgcn_udot4(nz[3], kc.C2, __builtin_amdgcn_udot4(nz[2], kc.C1, 0u, false), false);
+    const u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
+    const u32 prevP = from_prev_lane(P16, 0u);
+    u32 del = ((P16 << 2) | (prevP >> 14)) & 0xFFFFu;
+    if (lane == 0u) del |= lowmask(d);
+    const u32 K = lane < kOwnLanes ? (~del & 0xFFFFu) : ((prevP >> 15) & 1u);
+    if (__builtin_amdgcn_ballot_w64((P16 & NZ16) != 0u) & kOwned) return kNotFast;
+    return wave_sum((u32)__builtin_popcount(K));
+}
+
 __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_t* __restrict__ in,
                                                                     const uint64_t* __restrict__ in_off,
                                                                     const uint64_t* __restrict__ in_len, u32 n,
@@ -292,9 +355,13 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_
                 const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
                 const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
                 if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
-                    const DecLen ln = dec_lengths(pr, d0);
-                    const u32 tot = owned_sum(ln.nout);
-                    const bool bad = owned_any(ln.serial_lane);
+                    u32 tot = (RLE_SEG_SUMFAST && !pr.tail) ? dec_count_literal(pr, d0, lane, kc) : kNotFast;
+                    bool bad = false;
+                    if (tot == kNotFast) {
+                        const DecLen ln = dec_lengths(pr, d0);
+                        tot = owned_sum(ln.nout);
+                        bad = owned_any(ln.serial_lane);
+                    }
                     c0 += tot; c1 += tot; c2 += tot;
                     badm |= bad ? 7u : 0u;
                     d0 = d1 = d2 = bfe(m63, 8u * d0, 8);

@@ -40,6 +40,11 @@ def test_segment_edge_sizes():
 
 def test_runs_and_phases_across_segments():
     xs = [bytes(3 * S + 5), b"\xff" * (2 * S + 2), b"9" * (2 * S + 7), b"3" * (S + 3), b"99" * S]
+    # a zero run from position 0 (its first tile must not pass for the inside of a run), whole tiles
+    # inside runs ending on and off tile edges (the summary's uniform-tile count)
+    xs += [bytes(S + 2000) + O.gen(1, 3, S), bytes(2 * S) + b"\x01" + bytes(S)]
+    for e in (1007, 1008, 1009, 2016, 2017, 5000):
+        xs.append(O.gen(1, e, 3000) + b"q" * (e + S) + O.gen(1, e + 1, S))
     for k in (1, 2, 5, 8, 9, 10, 17, 100):   # a run ending / starting k bytes around a segment edge
         xs.append(b"a" * (S - k) + b"b" * (2 * k + 9) + b"c" * 1000)
         xs.append(O.gen(1, k, S - k) + b"z" * (k + 40) + O.gen(3, k, S))
