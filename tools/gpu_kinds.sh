@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${1:-kinds}
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$TAG; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-for WL in k64_zero k64_random k64_runs50 k64_runs90 cfg1; do
+for WL in k64_zero k64_random k64_runs50 k64_runs90 dec64k cfg1; do
   timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/kt_$WL -o run -- python3 $R/tools/prof_driver.py --workload $WL --reps 5 > $O/kt_$WL.log 2>&1
   rc=$?; echo "kt $WL rc=$rc" >> $O/status; [ $rc -ne 0 ] && exit $rc
 done

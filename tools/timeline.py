@@ -3,7 +3,7 @@
 NAME=tl DEFS=-DRLE_TIMELINE=1; selected with RLE_MI355X_LIB).  Prints, in microseconds relative to
 the first wave's entry: the spread of wave entries, walk starts, the start of each tile, the ends,
 and per tile index the median interval between consecutive tile starts.
-usage: RLE_MI355X_LIB=.../librle_tl.so python tools/timeline.py [--workload cfg1]"""
+usage: RLE_MI355X_LIB=.../librle_tl.so python tools/timeline.py [--workload cfg1] [--n 256]"""
 import argparse
 import ctypes
 import os
@@ -20,6 +20,7 @@ import rle_mi355x as R  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="cfg1")
+ap.add_argument("--n", type=int, default=0, help="buffers (default: the workload's); e.g. 256 for lone waves")
 a = ap.parse_args()
 L = R.lib()
 L.rle_mi355x_timeline.restype = ctypes.c_int
@@ -91,7 +92,10 @@ def report(name, tl, n):
 
 
 torch.cuda.set_device(0)
-B = bench.Batch(bench.WORKLOADS[a.workload], 0, 1, torch.device("cuda", 0))
+wl = dict(bench.WORKLOADS[a.workload])
+if a.n:
+    wl["n"] = a.n
+B = bench.Batch(wl, 0, 1, torch.device("cuda", 0))
 s = torch.cuda.current_stream()
 B.encode(s)
 B.calibrate()
