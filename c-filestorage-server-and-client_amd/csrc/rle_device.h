@@ -146,18 +146,39 @@ __device__ __forceinline__ u32 lds_addr(const void* p) {
 // Loads and stores in asm: hipcc neither counts nor waits for them; vm_wait() is the only wait
 // for them.  Loads go straight to LDS (LDS-DMA: lane i's 16 bytes land at lds + 16 i), so no
 // VGPR is in flight that the compiler could copy or reuse before the data lands.
+#ifndef RLE_LD_NT   // 1: the tile loads carry the non-temporal hint (streamed input: experiment)
+#define RLE_LD_NT 0
+#endif
+#if RLE_LD_NT
+#define RLE_LD_BITS " nt"
+#else
+#define RLE_LD_BITS ""
+#endif
+template <bool kStream = false>
 __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
     u32 keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"   // earlier ds_reads of this slot have completed
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(voff), "s"(lds), "s"(rs)
-        : "memory");
+    if (kStream)
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"   // earlier ds_reads of this slot have completed
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %3, 0 offen" RLE_LD_BITS " lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(lds), "s"(rs)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"   // earlier ds_reads of this slot have completed
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(lds), "s"(rs)
+            : "memory");
 }
 #ifndef RLE_NOSTORE
 #define RLE_NOSTORE 0
@@ -170,18 +191,26 @@ __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
 #ifndef RLE_WT_BITS   // cache-policy bits of the write-through stores (experiments: "sc1 nt", "sc0 sc1")
 #define RLE_WT_BITS "sc1"
 #endif
+#ifndef RLE_ST_NT   // 1: the large launches' (write-back) stores carry the non-temporal hint (experiment)
+#define RLE_ST_NT 0
+#endif
+#if RLE_ST_NT
+#define RLE_WB_BITS " nt"
+#else
+#define RLE_WB_BITS ""
+#endif
 __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v, bool wt) {
     if (wt)
         asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen " RLE_WT_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
     else
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" RLE_WB_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
 // One 4-byte store (buffer_store_dword; offsets need not be aligned).
 __device__ __forceinline__ void vstore4(u32x4 rs, u32 voff, u32 v, bool wt) {
     if (wt)
         asm volatile("buffer_store_dword %0, %1, %2, 0 offen " RLE_WT_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
     else
-        asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen" RLE_WB_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
 
 // wait until at most n vector-memory ops are outstanding
@@ -228,8 +257,8 @@ struct Refill {
     bool look;   // kLook walks: lane 0 also loads the 16 bytes after the tile into the slot's tail
     __device__ __forceinline__ void operator()() const {
         if (on) {
-            dma_tile(rs, voff, lds);
-            if (look) dma_tile(rs, voff + kEncStep, lds + kSlot);
+            dma_tile<true>(rs, voff, lds);
+            if (look) dma_tile<true>(rs, voff + kEncStep, lds + kSlot);
         }
     }
 };
@@ -686,24 +715,19 @@ __device__ __forceinline__ u32 enc_tile_fast(const EncAn& a, const uint2 look, u
 // then a 3-periodic pattern: lane c forms staged chunk c (the partial chunk's bytes first) and
 // the flush stores it; the new partial chunk goes back to the staging.  Not for the last tile.
 __device__ __forceinline__ u32 rep_byte(u32 v) { return __builtin_amdgcn_perm(0u, v, 0u); }
-template <bool k64>
-__device__ __forceinline__ u32 enc_tile_run(const EncAn& a, u32 pos, u32 lane, uint8_t* stage, u32x4 rso,
-                                            EncState& st) {
-    constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;
-    constexpr u32 kStep = k64 ? kEncStep : kTileStep;
-    const bool owned = k64 || lane < kOwnLanes;
-    if (__builtin_amdgcn_ballot_w64((a.B & (lane == 0u ? 0xFFFEu : 0xFFFFu)) != 0u && owned)) return kNotFast;
-    const u32 rs = (readlane(a.B, 0) & 1u) ? pos : st.rs;     // the run's start
-    const u32 f = pos + (9u - (pos - rs) % 9u) % 9u;          // first token start in the tile
-    const u32 ns = (pos + kStep - f + 8u) / 9u;               // token starts in the tile (>= 1)
+// The output of `span` bytes that are one run (from rs, run start; v its byte; ext: run bytes past
+// the span, up to 8), after the partial chunk staged so far.  One store round: span <= 2048 gives
+// at most 15 + 3 * 228 bytes, 44 chunks.
+__device__ __forceinline__ void enc_run_emit(u32 pos, u32 span, u32 rs, u32 ext, u32 v, u32 lane, uint8_t* stage,
+                                             u32x4 rso, EncState& st) {
+    const u32 f = pos + (9u - (pos - rs) % 9u) % 9u;          // first token start in the span
+    const u32 ns = (pos + span - f + 8u) / 9u;                // token starts in the span (>= 1)
     const u32 sl = f + 9u * (ns - 1u);
-    const u32 ext = (u32)__builtin_ctz((readlane(a.B24, kLast) >> 16) | 0x100u);   // run bytes past the tile
-    const u32 cl = pos + kStep + ext - sl < 9u ? pos + kStep + ext - sl : 9u;     // last token's count
+    const u32 cl = pos + span + ext - sl < 9u ? pos + span + ext - sl : 9u;     // last token's count
     const u32 tot = 3u * (ns - 1u) + (cl >= 2u ? 3u : 1u);
-    const u32 v = readlane(a.w[0], 0) & 0xFFu;
     const u32 rel0 = st.out_pos - st.flushed;
     const u32 rel = rel0 + tot, nfl = rel >> 4;
-    // lane c: staged chunk c = output bytes k = 16 c + i - rel0 of this tile (k < 0: the old partial)
+    // lane c: staged chunk c = output bytes k = 16 c + i - rel0 of this span (k < 0: the old partial)
     const u32 k0 = 16u * lane - rel0;                         // may wrap for lane 0
     const u32 ph = (16u * lane + 48u - rel0) % 3u;            // k0 mod 3
     const u32 vv = rep_byte(v), d9 = 0x39393939u;
@@ -754,21 +778,29 @@ __device__ __forceinline__ u32 enc_tile_run(const EncAn& a, u32 pos, u32 lane, u
     wave_lds_sync();
     st.flushed += 16u * nfl;
     st.out_pos += tot;
+}
+template <bool k64>
+__device__ __forceinline__ u32 enc_tile_run(const EncAn& a, u32 pos, u32 lane, uint8_t* stage, u32x4 rso,
+                                            EncState& st) {
+    constexpr u32 kLast = k64 ? 63u : kOwnLanes - 1u;
+    constexpr u32 kStep = k64 ? kEncStep : kTileStep;
+    const bool owned = k64 || lane < kOwnLanes;
+    if (__builtin_amdgcn_ballot_w64((a.B & (lane == 0u ? 0xFFFEu : 0xFFFFu)) != 0u && owned)) return kNotFast;
+    const u32 rs = (readlane(a.B, 0) & 1u) ? pos : st.rs;     // the run's start
+    const u32 ext = (u32)__builtin_ctz((readlane(a.B24, kLast) >> 16) | 0x100u);   // run bytes past the tile
+    enc_run_emit(pos, kStep, rs, ext, readlane(a.w[0], 0) & 0xFFu, lane, stage, rso, st);
     st.prev_top = readlane(a.top, kLast);
     const u32 i63 = readlane(a.incl, kLast);
     st.rs = i63 > st.rs ? i63 : st.rs;
     return 1u;
 }
 
+// One tile from its boundary analysis (enc_analyze_bounds): the fast paths when they apply, else
+// the general path.  Returns the store instructions issued.
 template <bool k64, bool kFast = false>
-__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
-                                        u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
-                                        const EncK& kc, const u32* elut = nullptr) {
-    RLE_STAMP(st.sp, 0);   // DMA wait + loop
-    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
-    const uint2 look = k64 ? *reinterpret_cast<const uint2*>(cslot + kSlot) : uint2{0u, 0u};
-    next();   // the slot is free once read
-    EncAn an = enc_analyze_bounds<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, kc);
+__device__ __forceinline__ u32 enc_tile_an(EncAn an, const uint2 look, u32 pos, u32 Ud, u32 Uo, u32 lane,
+                                           uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st, const EncK& kc,
+                                           const u32* elut) {
     if (kFast && RLE_ENC_FAST && !st.head) {
         if (pos + (k64 ? kEncStep : kTileStep) < Uo) {
             u32 r = enc_tile_run<k64>(an, pos, lane, stage, rso, st);
@@ -869,6 +901,219 @@ __device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next
     st.rs = i63 > st.rs ? i63 : st.rs;
     RLE_STAMP(st.sp, 5);   // partial-chunk move, state
     return rounds;
+}
+template <bool k64, bool kFast = false>
+__device__ __forceinline__ u32 enc_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 Ud, u32 Uo,
+                                        u32 lane, uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st,
+                                        const EncK& kc, const u32* elut = nullptr) {
+    RLE_STAMP(st.sp, 0);   // DMA wait + loop
+    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    const uint2 look = k64 ? *reinterpret_cast<const uint2*>(cslot + kSlot) : uint2{0u, 0u};
+    next();   // the slot is free once read
+    const EncAn an = enc_analyze_bounds<k64>(cur, look, pos, Ud, Uo, lane, st.prev_top, kc);
+    return enc_tile_an<k64, kFast>(an, look, pos, Ud, Uo, lane, stage, dst, rso, st, kc, elut);
+}
+
+__device__ __forceinline__ u32 max_u(u32 a, u32 b) { return a > b ? a : b; }
+// ---------------------------------------------------------------- two tiles per step (1024-byte tiles)
+// A lone wave spends ~0.9 us per tile (r3n timelines: one wave per SIMD), about 12 cycles per
+// instruction: each tile is one dependent chain (LDS read, SWAR, DPP scans, readlanes, stores).
+// The tiles of a buffer depend on each other only through a few scalars (the byte before the
+// tile, the entering run start, the output offset), so a step takes two tiles: both analyses and
+// both offset scans are independent, and the compiler interleaves them.  Pair forms:
+//  * run pair: both tiles one run (a boundary at most at the first byte) -- one run emission over
+//    2048 bytes (enc_run_emit);
+//  * literal pair: both tiles literal (enc_tile_fast's conditions), the second possibly the
+//    buffer's last tile (kTail1: its stores clipped at C, its last dword stored again).
+// Anything else runs the two tiles one after the other from their analyses (enc_tile_an).
+#ifndef RLE_ENC_PAIR   // 0: one tile per step (the walk of round 2)
+#define RLE_ENC_PAIR 1
+#endif
+// literal output of one tile: the lane's bytes with the '2's inserted (enc_tile_fast's body)
+struct EncLit {
+    u32 out[5];
+    u32 nout, j2;
+};
+__device__ __forceinline__ void enc_lit_insert(const u32* elut, const u32* in, u32 i, u32* out) {
+    typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+    const u32 k2 = 0x32323232u;
+    const u32* e = elut + i * kInsStride;
+    const u32x2 e01 = *reinterpret_cast<const u32x2*>(e), e23 = *reinterpret_cast<const u32x2*>(e + 2),
+                e45 = *reinterpret_cast<const u32x2*>(e + 4);
+    out[0] = __builtin_amdgcn_perm(in[0], k2, e01.x);
+    out[1] = __builtin_amdgcn_perm(in[1], __builtin_amdgcn_perm(in[0], k2, 0x07060100u), e01.y);
+    out[2] = __builtin_amdgcn_perm(in[2], __builtin_amdgcn_perm(in[1], k2, 0x07060100u), e23.x);
+    out[3] = __builtin_amdgcn_perm(in[3], __builtin_amdgcn_perm(in[2], k2, 0x07060100u), e23.y);
+    out[4] = __builtin_amdgcn_perm(in[4], __builtin_amdgcn_perm(in[3], k2, 0x07060100u), e45.x);
+}
+// P (pair starts) and the lane's output count of a literal k64 tile; vm: valid positions
+__device__ __forceinline__ u32 enc_lit_count(const EncAn& a, u32 vm, u32& P) {
+    const u32 C18 = ~a.B24 & 0x3FFFFu;
+    P = a.B & ~(a.B24 >> 1) & vm;
+    return (u32)__builtin_popcount(vm) - (C18 & 1u) + ((P >> 15) & 1u) + (u32)__builtin_popcount(P);
+}
+__device__ __forceinline__ bool enc_lit_reject(const EncAn& a, u32 vm) {
+    const u32 C18 = ~a.B24 & 0x3FFFFu;
+    const u32 P = a.B & ~(a.B24 >> 1) & vm;
+    return (C18 & (C18 >> 1)) != 0u || __builtin_popcount(P) > 2;
+}
+// first insertion pass (the second, for lanes with two pairs, is the caller's: enc_lit_second)
+__device__ __forceinline__ EncLit enc_lit_first(const EncAn& a, const uint2 look, u32 lane, u32 P, u32 nout,
+                                                const u32* elut) {
+    EncLit r;
+    const u32* w = a.w;
+    const u32 del0 = (~a.B24) & 1u;
+    const u32 nw0 = from_next_lane(w[0], 0u);
+    const u32 s4 = lane == 63u ? look.x : nw0;
+    const u32 sh = 8u * del0;
+    const u32 Sp[5] = {alignbyte(w[1], w[0], del0), alignbyte(w[2], w[1], del0), alignbyte(w[3], w[2], del0),
+                       alignbyte(s4, w[3], del0), s4 >> sh};
+    const u32 j1 = (u32)__builtin_ctz(P | 0x10000u), j2 = (u32)__builtin_ctz((P & (P - 1u)) | 0x10000u);
+    enc_lit_insert(elut, Sp, j1 < 16u ? j1 + 2u - del0 : 0u, r.out);
+    r.nout = nout;
+    r.j2 = j2 < 16u ? j2 + 3u - del0 : 0u;
+    return r;
+}
+__device__ __forceinline__ void enc_lit_second(EncLit& r, const u32* elut) {
+    const u32 o1[5] = {r.out[0], r.out[1], r.out[2], r.out[3], r.out[4]};
+    enc_lit_insert(elut, o1, r.j2, r.out);
+}
+// the stores of one literal tile whose output starts at base (va: first 16 bytes; vb: last 16)
+__device__ __forceinline__ void enc_lit_store(const EncLit& r, u32 base, u32 oincl, u32x4 rso, bool wt) {
+    const u32 n0 = from_next_lane(r.out[0], 0u);
+    u32x4 va;
+    va.x = r.out[0]; va.y = r.out[1]; va.z = r.out[2];
+    va.w = __builtin_amdgcn_perm(n0, r.out[3], r.nout >= 16u ? 0x03020100u : 0x04020100u);
+    const u32 o = base + oincl - r.nout;
+    vstore(rso, r.nout ? o : kOOB, va, wt);
+}
+__device__ __forceinline__ void enc_lit_store_b(const EncLit& r, u32 base, u32 oincl, u32x4 rso, bool wt) {
+    const u32 o = base + oincl - r.nout;
+    const u32 b = r.nout - 16u;
+    u32x4 vb;
+    vb.x = alignbyte(r.out[1], r.out[0], b); vb.y = alignbyte(r.out[2], r.out[1], b);
+    vb.z = alignbyte(r.out[3], r.out[2], b); vb.w = alignbyte(r.out[4], r.out[3], b);
+    vstore(rso, r.nout > 16u ? o + b : kOOB, vb, wt);
+}
+
+// Two 1024-byte tiles (k64 walks: buffers up to 16 KiB) at pos and pos + 1024; slot A holds the
+// first, slot B the second.  Returns the store instructions issued after the refills.
+template <bool kFast>
+__device__ __forceinline__ u32 enc_pair(const uint8_t* slotA, const uint8_t* slotB, const Refill& nxA,
+                                        const Refill& nxB, u32 pos, u32 U, u32 lane, uint8_t* stage, uint8_t* dst,
+                                        u32x4 rso, EncState& st, const EncK& kc, const u32* elut) {
+    const u32x4 curA = *reinterpret_cast<const u32x4*>(slotA + 16u * lane);
+    const uint2 lookA = *reinterpret_cast<const uint2*>(slotA + kSlot);
+    const u32x4 curB = *reinterpret_cast<const u32x4*>(slotB + 16u * lane);
+    const uint2 lookB = *reinterpret_cast<const uint2*>(slotB + kSlot);
+    nxA();
+    nxB();
+    const u32 pos1 = pos + kEncStep;
+    const EncAn a0 = enc_analyze_bounds<true>(curA, lookA, pos, U, U, lane, st.prev_top, kc);
+    // the byte before tile 1: tile 0's last byte (lane 63's top), from the data
+    const EncAn a1 = enc_analyze_bounds<true>(curB, lookB, pos1, U, U, lane, readlane(curA.w & 0xFF000000u, 63), kc);
+    if (kFast && RLE_ENC_FAST && !st.head) {
+        const bool last1 = pos1 + kEncStep >= U;   // tile 1 is the buffer's last tile
+        // run pair: both tiles one run (tile 1's first byte continues tile 0's last)
+        if (!last1) {
+            const bool brk = (a0.B & (lane == 0u ? 0xFFFEu : 0xFFFFu)) != 0u || a1.B != 0u;
+            if (!__builtin_amdgcn_ballot_w64(brk)) {
+                const u32 rs = (readlane(a0.B, 0) & 1u) ? pos : st.rs;
+                const u32 ext = (u32)__builtin_ctz((readlane(a1.B24, 63) >> 16) | 0x100u);
+                enc_run_emit(pos, 2u * kEncStep, rs, ext, readlane(a0.w[0], 0) & 0xFFu, lane, stage, rso, st);
+                st.prev_top = readlane(a1.top, 63);
+                const u32 i63 = readlane(a1.incl, 63);
+                st.rs = i63 > st.rs ? i63 : st.rs;
+                return 1u;
+            }
+        }
+        // literal pair
+        const u32 vm1 = last1 ? a1.validm : 0xFFFFu;
+        const bool rej = enc_lit_reject(a0, 0xFFFFu) || enc_lit_reject(a1, vm1);
+        const u32 rs1 = max_u(readlane(a0.incl, 63), st.rs);   // the run holding tile 1's byte before
+        if (!__builtin_amdgcn_ballot_w64(rej) && !((readlane(~a0.B24, 0) & 1u) && st.rs + 1u != pos) &&
+            !((readlane(~a1.B24, 0) & 1u) && rs1 + 1u != pos1)) {
+            u32 P0, P1;
+            const u32 n0 = enc_lit_count(a0, 0xFFFFu, P0), n1 = enc_lit_count(a1, vm1, P1);
+            const u32 oi0 = wave_scan_incl(n0, 0u, OpAdd()), oi1 = wave_scan_incl(n1, 0u, OpAdd());
+            const u32 t0 = readlane(oi0, 63), t1 = readlane(oi1, 63);
+            if (!last1 || t1 >= 4u) {
+                EncLit L0 = enc_lit_first(a0, lookA, lane, P0, n0, elut);
+                EncLit L1 = enc_lit_first(a1, lookB, lane, P1, n1, elut);
+                if (__builtin_amdgcn_ballot_w64(L0.j2 != 0u || L1.j2 != 0u)) {
+                    enc_lit_second(L0, elut);
+                    enc_lit_second(L1, elut);
+                }
+                u32 rounds = 2u;
+                const u32 rel0 = st.out_pos - st.flushed;
+                const u32 base0 = st.out_pos, base1 = st.out_pos + t0, C = base1 + t1;
+                // a last pair clips every store at C (tile 0's reach past its output too)
+                const u32x4 rsc = u32x4{rso.x, rso.y, uniform(last1 ? C : rso.z), rso.w};
+                asm volatile("s_nop 4" ::: "memory");   // (the descriptor word is fresh)
+                if (rel0) {   // a general tile's partial chunk (its bytes past rel0 are rewritten below)
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16u);
+                    vstore(rsc, lane == 0u ? st.flushed : kOOB, v, st.wt);
+                    ++rounds;
+                }
+                enc_lit_store(L0, base0, oi0, rsc, st.wt);
+                if (__builtin_amdgcn_ballot_w64(n0 > 16u)) {
+                    enc_lit_store_b(L0, base0, oi0, rsc, st.wt);
+                    ++rounds;
+                }
+                enc_lit_store(L1, base1, oi1, rsc, st.wt);
+                if (__builtin_amdgcn_ballot_w64(n1 > 16u)) {
+                    enc_lit_store_b(L1, base1, oi1, rsc, st.wt);
+                    ++rounds;
+                }
+                if (last1) {
+                    // tile 1's last 4 output bytes as one dword ending at C (enc_tile_fast<kTail>)
+                    const u32 nout = n1;
+                    const u32* out = L1.out;
+                    const u32 s4b = nout - 4u, qd = s4b >> 2;
+                    const u32 lo = qd == 0u ? out[0] : qd == 1u ? out[1] : qd == 2u ? out[2] : out[3];
+                    const u32 hi = qd == 0u ? out[1] : qd == 1u ? out[2] : qd == 2u ? out[3] : out[4];
+                    const u32 T4 = alignbyte(hi, lo, s4b & 3u);
+                    const u32 Tp = from_prev_lane(T4, 0u);
+                    const u32 T = nout >= 4u ? T4 : alignbyte(out[0], Tp, nout);
+                    const uint64_t has = __builtin_amdgcn_ballot_w64(nout != 0u);
+                    const u32 lastl = 63u - (u32)__builtin_clzll(has);
+                    vstore4(rsc, lane == lastl ? C - 4u : kOOB, T, st.wt);
+                    ++rounds;
+                }
+                st.out_pos = C;
+                st.flushed = C;
+                st.prev_top = readlane(a1.top, 63);
+                const u32 i63 = readlane(a1.incl, 63);
+                st.rs = i63 > rs1 ? i63 : rs1;
+                return rounds;
+            }
+        }
+    }
+    // one after the other
+    const u32 r0 = enc_tile_an<true, kFast>(a0, lookA, pos, U, U, lane, stage, dst, rso, st, kc, elut);
+    const u32 r1 = enc_tile_an<true, kFast>(a1, lookB, pos1, U, U, lane, stage, dst, rso, st, kc, elut);
+    return r0 + r1;
+}
+// The k64 walk two tiles per step (slots A, B; the last tile of an odd count alone, slot A).  As
+// walk_tiles: the wait before a step leaves only the previous step's stores in flight.
+template <class Pair, class Single>
+__device__ __forceinline__ void walk_pairs(u32x4 rs, u32 ntiles, u32 lane, const uint8_t* slots, Pair pair,
+                                           Single single) {
+    constexpr u32 kStride = kEncSlot;
+    const u32 lo = 16u * lane;
+    const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kStride;
+    const bool look = lane == 0u;
+    walk_prime<kEncStep, true>(rs, 0u, ntiles, lane, slots);
+    u32 p1 = 0, t = 0;
+    for (; t + 1u < ntiles; t += 2u) {
+        vm_wait(p1);
+        p1 = pair(t, slots, slots + kStride, Refill{rs, (t + 2u) * kEncStep + lo, l0, t + 2u < ntiles, look},
+                  Refill{rs, (t + 3u) * kEncStep + lo, l1, t + 3u < ntiles, look});
+    }
+    if (t < ntiles) {
+        vm_wait(p1);
+        single(t, slots, Refill{rs, 0u, l0, false, look});
+    }
 }
 
 // ================================================================ DECODE

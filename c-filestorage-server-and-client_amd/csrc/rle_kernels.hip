@@ -134,13 +134,25 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     stagger();
     tl_mark(b, 1, lane);
     // 1024-byte tiles where they save a tile, up to kEncSmall (rle_device.h, enc_tile<true>)
-    if (enc_ntiles_for(U) < ntiles_for(U) && U <= kEncSmall)
-        walk_tiles<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
-                                   [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                                       tl_mark(b, 2u + t, lane);
-                                       return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
-                                   });
-    else
+    if (enc_ntiles_for(U) < ntiles_for(U) && U <= kEncSmall) {
+        if (RLE_ENC_PAIR)   // two tiles per step (rle_device.h enc_pair)
+            walk_pairs(rsi, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
+                       [&](u32 t, const uint8_t* sa, const uint8_t* sb, const Refill& na, const Refill& nb) {
+                           tl_mark(b, 2u + t, lane);
+                           tl_mark(b, 3u + t, lane);
+                           return enc_pair<true>(sa, sb, na, nb, t * kEncStep, U, lane, stage, dst, rso, st, kc, elut);
+                       },
+                       [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                           tl_mark(b, 2u + t, lane);
+                           return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
+                       });
+        else
+            walk_tiles<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
+                                       [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                                           tl_mark(b, 2u + t, lane);
+                                           return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
+                                       });
+    } else
         walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
             tl_mark(b, 2u + t, lane);
             return enc_tile<false, true>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc, elut);

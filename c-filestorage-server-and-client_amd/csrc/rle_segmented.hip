@@ -34,6 +34,9 @@ constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the w
 #ifndef RLE_SEG_FAST   // the write passes take the fast tile paths (round 3); 0: general path only
 #define RLE_SEG_FAST 1
 #endif
+#ifndef RLE_SEG_REVERSE   // 1: the write passes take the segments last-summarised first (cache reuse: experiment)
+#define RLE_SEG_REVERSE 0
+#endif
 #ifndef RLE_SEG_SUMFAST   // the summaries count uniform / literal tiles without the full analysis (round 3)
 #define RLE_SEG_SUMFAST 1
 #endif
@@ -48,9 +51,14 @@ __device__ __forceinline__ u32 len32(uint64_t n) { return n > kMaxBufferBytes ? 
 
 // seg_first[i] = segments of buffers < i; seg_first[n] = total.  One workgroup.
 __global__ __launch_bounds__(1024) void seg_plan_kernel(const uint64_t* __restrict__ len, u32 n, u32 sb,
-                                                        u32* __restrict__ seg_first) {
+                                                        u32* __restrict__ seg_first, u32* __restrict__ sflag,
+                                                        u32 maxseg, u32* __restrict__ ticket) {
     __shared__ u32 part[1024];
     const u32 t = threadIdx.x;
+    // (fused kernels) every segment's publication flag cleared, the ticket counter at 0
+    if (sflag)
+        for (u32 i = t; i < maxseg; i += 1024u) sflag[i] = 0u;
+    if (ticket && t == 0u) *ticket = 0u;
     const u32 per = (n + 1023u) / 1024u;
     const u32 b0 = t * per < n ? t * per : n;
     const u32 b1 = b0 + per < n ? b0 + per : n;
@@ -106,6 +114,66 @@ __device__ __forceinline__ u32 enc_piece_count(u32 L0, u32 q, u32 cont) {
     return 3u * n - ((last_is_start && !cont) ? 2u : 0u);
 }
 
+// One segment's encode summary (L0, lb + 1 or 0, rest, cont; see the top of this file): a walk over
+// its tiles, analysis only.  U > 0, src 16-byte aligned.
+__device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u32 p0, u32 p1, u32 lane,
+                                                   const uint8_t* slots) {
+    const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+    u32 prev_top = p0 ? (u32)src[p0 - 1u] << 24 : 0u;
+    u32 rs = p0, fb = kNone, lb = kNone, rest = 0;
+    const EncK kc = enc_k();
+    walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
+        nx();
+        const u32 pos = p0 + t * kTileStep;
+        // (tried only when the run entering the tile is already 16 bytes long, a scalar test
+        // that keeps the check off random and short-run tiles)
+        if (RLE_SEG_SUMFAST && pos != 0u && pos - rs >= 16u && pos + kTileStep < p1) {
+            // a tile inside a run (every byte, and the first lookahead byte, equal to the byte
+            // before the tile; never the buffer's first tile, whose position 0 is a boundary
+            // whatever its byte): no boundary, so fb, lb and rs stay; the tokens count only past
+            // the segment's first boundary, all 3-byte (the run goes on), one every 9 bytes
+            // from the run start rs.  About 10 VALU against enc_analyze's ~75.
+            const u32 v = uniform(readlane(cur.x, 0)) & 0xFFu;
+            if ((prev_top >> 24) == v) {
+                const u32 vrep = v * 0x01010101u;
+                const bool diff = lane < kOwnLanes
+                                      ? ((cur.x ^ vrep) | (cur.y ^ vrep) | (cur.z ^ vrep) | (cur.w ^ vrep)) != 0u
+                                      : ((cur.x ^ vrep) & 0xFFu) != 0u;
+                if (!__builtin_amdgcn_ballot_w64(diff)) {
+                    if (fb != kNone) {
+                        const u32 f = pos + (9u - (pos - rs) % 9u) % 9u;   // first token start
+                        if (f < pos + kTileStep) rest += 3u * ((pos + kTileStep - 1u - f) / 9u + 1u);
+                    }
+                    return 0u;
+                }
+            }
+        }
+        const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, pos, U, p1, lane, prev_top, rs, kc);
+        // run boundaries inside the segment: the first one (L0) and the last one (lb)
+        const u32 Bo = an.B & an.validm;
+        const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
+        if (bl) {
+            const u32 fl = (u32)__builtin_ctzll(bl), ll = 63u - (u32)__builtin_clzll(bl);
+            const u32 first = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), fl);
+            const u32 last = readlane(an.p0 + 31u - (u32)__builtin_clz(Bo | 1u), ll);
+            if (fb == kNone) fb = first;
+            lb = last;
+        }
+        // tokens at or after the first boundary do not depend on the entering run phase
+        u32 fbm = 0u;
+        if (fb != kNone) fbm = fb <= an.p0 ? 0xFFFFu : (fb >= an.p0 + 16u ? 0u : ~lowmask(fb - an.p0) & 0xFFFFu);
+        rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
+        prev_top = readlane(an.top, kOwnLanes - 1u);
+        const u32 i63 = readlane(an.incl, kOwnLanes - 1u);
+        rs = i63 > rs ? i63 : rs;
+        return 0u;
+    });
+    const u32 L0 = fb == kNone ? p1 - p0 : fb - p0;
+    const u32 cont = (fb == kNone && p1 < U && src[p1] == src[p1 - 1u]) ? 1u : 0u;
+    return make_uint4(L0, lb == kNone ? 0u : lb + 1u, rest, cont);
+}
+
 __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_t* __restrict__ in,
                                                                     const uint64_t* __restrict__ in_off,
                                                                     const uint64_t* __restrict__ in_len, u32 n,
@@ -124,66 +192,34 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_
         const uint8_t* src = in + in_off[b];
         uint4 res = make_uint4(0u, 0u, 0u, 0u);
         if (U64 > 0 && U64 <= kMaxBufferBytes && !((uintptr_t)src & 15u)) {
-            const u32 U = (u32)U64;
             u32 p0, p1;
-            seg_range(g - s0, nseg, U, sb, p0, p1);
-            const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
-            u32 prev_top = p0 ? (u32)src[p0 - 1u] << 24 : 0u;
-            u32 rs = p0, fb = kNone, lb = kNone, rest = 0;
-            const EncK kc = enc_k();
-            walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
-                nx();
-                const u32 pos = p0 + t * kTileStep;
-                // (tried only when the run entering the tile is already 16 bytes long, a scalar test
-                // that keeps the check off random and short-run tiles)
-                if (RLE_SEG_SUMFAST && pos != 0u && pos - rs >= 16u && pos + kTileStep < p1) {
-                    // a tile inside a run (every byte, and the first lookahead byte, equal to the byte
-                    // before the tile; never the buffer's first tile, whose position 0 is a boundary
-                    // whatever its byte): no boundary, so fb, lb and rs stay; the tokens count only past
-                    // the segment's first boundary, all 3-byte (the run goes on), one every 9 bytes
-                    // from the run start rs.  About 10 VALU against enc_analyze's ~75.
-                    const u32 v = uniform(readlane(cur.x, 0)) & 0xFFu;
-                    if ((prev_top >> 24) == v) {
-                        const u32 vrep = v * 0x01010101u;
-                        const bool diff = lane < kOwnLanes
-                                              ? ((cur.x ^ vrep) | (cur.y ^ vrep) | (cur.z ^ vrep) | (cur.w ^ vrep)) != 0u
-                                              : ((cur.x ^ vrep) & 0xFFu) != 0u;
-                        if (!__builtin_amdgcn_ballot_w64(diff)) {
-                            if (fb != kNone) {
-                                const u32 f = pos + (9u - (pos - rs) % 9u) % 9u;   // first token start
-                                if (f < pos + kTileStep) rest += 3u * ((pos + kTileStep - 1u - f) / 9u + 1u);
-                            }
-                            return 0u;
-                        }
-                    }
-                }
-                const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, pos, U, p1, lane, prev_top, rs, kc);
-                // run boundaries inside the segment: the first one (L0) and the last one (lb)
-                const u32 Bo = an.B & an.validm;
-                const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
-                if (bl) {
-                    const u32 fl = (u32)__builtin_ctzll(bl), ll = 63u - (u32)__builtin_clzll(bl);
-                    const u32 first = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), fl);
-                    const u32 last = readlane(an.p0 + 31u - (u32)__builtin_clz(Bo | 1u), ll);
-                    if (fb == kNone) fb = first;
-                    lb = last;
-                }
-                // tokens at or after the first boundary do not depend on the entering run phase
-                u32 fbm = 0u;
-                if (fb != kNone) fbm = fb <= an.p0 ? 0xFFFFu : (fb >= an.p0 + 16u ? 0u : ~lowmask(fb - an.p0) & 0xFFFFu);
-                rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
-                prev_top = readlane(an.top, kOwnLanes - 1u);
-                const u32 i63 = readlane(an.incl, kOwnLanes - 1u);
-                rs = i63 > rs ? i63 : rs;
-                return 0u;
-            });
-            const u32 L0 = fb == kNone ? p1 - p0 : fb - p0;
-            const u32 cont = (fb == kNone && p1 < U && src[p1] == src[p1 - 1u]) ? 1u : 0u;
-            res = make_uint4(L0, lb == kNone ? 0u : lb + 1u, rest, cont);
+            seg_range(g - s0, nseg, (u32)U64, sb, p0, p1);
+            res = enc_seg_summarize(src, (u32)U64, p0, p1, lane, slots);
         }
         if (lane == 0) summ[g] = res;
     }
+}
+
+// The carried state of an encode scan over a buffer's segments: max (lb + 1) so far, and the output
+// offset.  One window of up to 64 consecutive segments (lane i: segment base + i, summary sm, first
+// position p0), entered with c: each lane's entering run start and output offset; c advances past
+// the window.  Shared by the per-buffer scan and the fused kernel's look-back.
+struct EncCarry {
+    u32 lb1, off;
+};
+__device__ __forceinline__ uint2 enc_seg_window(uint4 sm, bool valid, u32 p0, EncCarry& c) {
+    const u32 incl = wave_scan_incl(valid ? sm.y : 0u, 0u, OpMax());
+    const u32 ex = from_prev_lane(incl, 0u);
+    const u32 rsp1 = ex > c.lb1 ? ex : c.lb1;
+    const u32 rs = rsp1 ? rsp1 - 1u : 0u;
+    const u32 piece = (valid && p0 > 0u) ? enc_piece_count(sm.x, mod9(p0 - 1u - rs), sm.w) : 0u;
+    const u32 cnt = valid ? piece + sm.z : 0u;
+    const u32 oincl = wave_scan_incl(cnt, 0u, OpAdd());
+    const uint2 r = make_uint2(rs, c.off + oincl - cnt);
+    const u32 i63 = readlane(incl, 63);
+    c.lb1 = i63 > c.lb1 ? i63 : c.lb1;
+    c.off += readlane(oincl, 63);
+    return r;
 }
 
 // one wave per buffer: entering run start and output offset of every segment, C of the buffer
@@ -214,29 +250,38 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_scan_kernel(const uint8_t* 
         }
         return;
     }
-    u32 carry_lb = 0, carry_off = 0;   // max (lb + 1) so far; output offset
+    EncCarry c{0u, 0u};
     for (u32 base = s0; base < s1; base += kWave) {
         const u32 g = base + lane;
         const bool valid = g < s1;
         const uint4 sm = valid ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
-        const u32 p0 = (g - s0) * sb;
-        const u32 incl = wave_scan_incl(sm.y, 0u, OpMax());
-        const u32 ex = from_prev_lane(incl, 0u);
-        const u32 rsp1 = ex > carry_lb ? ex : carry_lb;
-        const u32 rs = rsp1 ? rsp1 - 1u : 0u;
-        const u32 piece = (valid && p0 > 0u) ? enc_piece_count(sm.x, mod9(p0 - 1u - rs), sm.w) : 0u;
-        const u32 cnt = valid ? piece + sm.z : 0u;
-        const u32 oincl = wave_scan_incl(cnt, 0u, OpAdd());
-        if (valid) plan[g] = make_uint2(rs, carry_off + oincl - cnt);
-        const u32 i63 = readlane(incl, 63);
-        carry_lb = i63 > carry_lb ? i63 : carry_lb;
-        carry_off += readlane(oincl, 63);
+        const uint2 pl = enc_seg_window(sm, valid, (g - s0) * sb, c);
+        if (valid) plan[g] = pl;
     }
     if (lane == 0) {
-        out_len[b] = carry_off;
+        out_len[b] = c.off;
         if (status) status[b] = RLE_STATUS_OK;
         bflag[b] = 0u;
     }
+}
+
+// One segment's output: the tile walk from its entering run start rs and output offset off.
+__device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, u32 U, u32 p0, u32 p1, u32 rs,
+                                              u32 off, u32 lane, const uint8_t* slots, uint8_t* stage,
+                                              const u32* elut) {
+    const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U + U / 2u);
+    EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, false, {}};
+    const EncK kc = enc_k();
+    walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        // the fast tile paths (round 3; until then only the one-wave kernels took them): past the
+        // segment's shared first chunk and before its last tile, as in a one-wave walk
+        return enc_tile<false, RLE_SEG_FAST>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc, elut);
+    });
+    // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past this
+    // segment's output and nothing before it
+    if (lane >= st.head && lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
+    wave_lds_sync();
 }
 
 __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t* __restrict__ in,
@@ -258,7 +303,8 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
-    for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
+    for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
+        const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
         const u32 b = seg_buffer(seg_first, n, g);
         if (uniform(bflag[b])) continue;
         const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
@@ -268,20 +314,150 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         u32 p0, p1;
         seg_range(g - s0, nseg, U, sb, p0, p1);
         const uint2 pl = plan[g];
-        const u32 rs = uniform(pl.x), off = uniform(pl.y);
-        const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
-        const u32x4 rso = make_rsrc(dst, U + U / 2u);
-        EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, false, {}};
-        const EncK kc = enc_k();
-        walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            // the fast tile paths (round 3; until then only the one-wave kernels took them): past the
-            // segment's shared first chunk and before its last tile, as in a one-wave walk
-            return enc_tile<false, RLE_SEG_FAST>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc, elut);
-        });
-        // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past this
-        // segment's output and nothing before it
-        if (lane >= st.head && lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
-        wave_lds_sync();
+        enc_seg_write(src, dst, U, p0, p1, uniform(pl.x), uniform(pl.y), lane, slots, stage, elut);
+    }
+}
+
+// ---------------------------------------------------------------- fused single-pass encode
+// One launch after the plan (SURVEY.md §5's single-pass form, with a decoupled look-back carry):
+// waves take segments in ticket order (a global counter), summarise their segment, publish the
+// summary (flag 1), derive their entering state from the published summaries and inclusive states
+// of the segments before them in the same buffer, publish their own inclusive state (flag 2), and
+// write their output at once: the segment's bytes are read a second time right after the first,
+// while they are still in the caches, and no separate scan launch waits for the whole batch.
+// Progress: a wave waits only on segments holding earlier tickets, whose waves are running and
+// never wait on later ones, so the earliest unfinished segment always advances.  The wait is
+// still bounded (kSpinMax polls); a wave that runs out publishes and marks its buffer
+// RLE_STATUS_INTERNAL instead of hanging (never seen; tests check the status is clean).
+constexpr u32 kSpinMax = 1u << 20;
+constexpr u32 kFlagAgg = 1u, kFlagIncl = 2u;
+// The hand-off follows MI355X_MICROARCH.md's write-through form (per-XCD L2s are not coherent, and
+// an agent release fence would write back the XCD's whole dirty L2 after every segment): the
+// publishing lane stores every payload word and the flag write-through (relaxed agent-scope atomic
+// stores: `sc1`), with `s_waitcnt vmcnt(0)` between them; readers poll the flag and read the
+// payload with `sc1` loads (relaxed agent-scope atomic loads), never plain or scalar-cache loads.
+__device__ __forceinline__ u32 ld_relaxed(const u32* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(u32* p, u32 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 ld_relaxed4(const uint4* p) {
+    const u32* w = reinterpret_cast<const u32*>(p);
+    return make_uint4(ld_relaxed(w), ld_relaxed(w + 1), ld_relaxed(w + 2), ld_relaxed(w + 3));
+}
+// (one lane) payload, drain, flag
+__device__ __forceinline__ void publish(uint4* slot, uint4 v, u32* flag, u32 f) {
+    u32* w = reinterpret_cast<u32*>(slot);
+    st_relaxed(w, v.x);
+    st_relaxed(w + 1, v.y);
+    st_relaxed(w + 2, v.z);
+    st_relaxed(w + 3, v.w);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_relaxed(flag, f);
+}
+// The first segment this wave must combine forward: j + 1 for the nearest j in [s0, g) whose
+// inclusive state is published, or s0 (the buffer's start state) when none is; on return every
+// segment in [result, g) has published its summary.  Windows of 64 flags, nearest first.
+__device__ __forceinline__ u32 seg_lookback(u32 g, u32 s0, const u32* sflag, u32 lane, bool& late) {
+    u32 hi = g;
+    for (;;) {
+        const u32 lo = hi - s0 > kWave ? hi - kWave : s0;
+        const bool valid = lane < hi - lo;
+        const u32 j = valid ? hi - 1u - lane : hi - 1u;
+        u32 f = valid ? ld_relaxed(sflag + j) : kFlagAgg;
+        u32 polls = 0;
+        while (__builtin_amdgcn_ballot_w64(f == 0u)) {
+            if (++polls > kSpinMax) {
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            if (f == 0u) f = ld_relaxed(sflag + j);
+        }
+        const uint64_t m2 = __builtin_amdgcn_ballot_w64(valid && f == kFlagIncl);
+        if (m2) return hi - (u32)__builtin_ctzll(m2);
+        if (lo == s0) return s0;
+        hi = lo;
+    }
+}
+
+__global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t* __restrict__ in,
+                                                                  const uint64_t* __restrict__ in_off,
+                                                                  const uint64_t* __restrict__ in_len,
+                                                                  uint8_t* __restrict__ out,
+                                                                  const uint64_t* __restrict__ out_off,
+                                                                  uint64_t* __restrict__ out_len,
+                                                                  uint32_t* __restrict__ status, u32 n,
+                                                                  const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                  uint4* __restrict__ summ, uint4* __restrict__ incl,
+                                                                  u32* __restrict__ sflag, u32* __restrict__ ticket) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kEncStage];
+    __shared__ __attribute__((aligned(16))) u32 elut[kInsWaveWords];   // enc_tile_fast's selectors
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    uint8_t* stage = stage_all + wid * kEncStage;
+    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    for (u32 k = threadIdx.x; k < kInsWaveWords; k += kSegBlock) elut[k] = kEncInsLut.s[k];
+    __syncthreads();
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (;;) {
+        u32 g = 0;
+        if (lane == 0) g = atomicAdd(ticket, 1u);
+        g = uniform(g);
+        if (g >= total) break;
+        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
+        const uint64_t U64 = in_len[b];
+        const uint8_t* src = in + in_off[b];
+        uint8_t* dst = out + out_off[b];
+        u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+        if (U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
+        if (bad || U64 == 0u) {   // the buffer's segments all skip (an empty buffer is one segment)
+            if (g == s0 && lane == 0) {
+                out_len[b] = 0;
+                if (status) status[b] = bad;
+            }
+            continue;
+        }
+        const u32 U = (u32)U64;
+        u32 p0, p1;
+        seg_range(g - s0, nseg, U, sb, p0, p1);
+        const uint4 sm = enc_seg_summarize(src, U, p0, p1, lane, slots);
+        if (lane == 0) publish(summ + g, sm, sflag + g, kFlagAgg);
+        // the state entering this segment: the nearest published inclusive state (or the buffer's
+        // start), then the summaries after it, 64 per window
+        bool late = false;
+        EncCarry c{0u, 0u};
+        u32 lateb = 0u;
+        if (g > s0) {
+            const u32 from = seg_lookback(g, s0, sflag, lane, late);
+            if (from > s0) {
+                const uint4 in4 = ld_relaxed4(incl + (from - 1u));
+                c = EncCarry{uniform(in4.x), uniform(in4.y)};
+                lateb = uniform(in4.z);
+            }
+            for (u32 base = from; base < g; base += kWave) {
+                const u32 j = base + lane;
+                const bool valid = j < g;
+                const uint4 smj = valid ? ld_relaxed4(summ + j) : make_uint4(0u, 0u, 0u, 0u);
+                enc_seg_window(smj, valid, (j - s0) * sb, c);
+            }
+        }
+        // this segment's own step (lane 0's window entry), published as its inclusive state
+        const uint2 mine = enc_seg_window(sm, lane == 0u, p0, c);
+        const u32 rs = uniform(mine.x), off = uniform(mine.y);
+        lateb |= late ? RLE_STATUS_INTERNAL : 0u;
+        if (lane == 0) {
+            publish(incl + g, make_uint4(c.lb1, c.off, lateb, 0u), sflag + g, kFlagIncl);
+            if (g + 1u == s1) {   // the buffer's last segment: C and the status
+                out_len[b] = c.off;
+                if (status) status[b] = lateb ? lateb : RLE_STATUS_OK;
+            }
+        }
+        enc_seg_write(src, dst, U, p0, p1, rs, off, lane, slots, stage, elut);
     }
 }
 
@@ -467,7 +643,8 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
-    for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
+    for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
+        const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
         const u32 b = seg_buffer(seg_first, n, g);
         const u32 flag = uniform(bflag[b]);
         if (flag & kFlagSkip) continue;
@@ -527,6 +704,9 @@ struct Carve {
     uint4* summ;
     uint2* plan;
     uint32_t* bflag;
+    uint32_t* sflag;    // fused kernels: per-segment publication flag
+    uint4* incl;        // fused kernels: per-segment inclusive state
+    uint32_t* ticket;   // fused kernels: segment ticket counter
     size_t bytes;
 };
 inline size_t al(size_t x) { return (x + 255u) & ~(size_t)255u; }
@@ -537,6 +717,9 @@ Carve carve(char* base, uint32_t n, uint32_t maxseg) {
     c.summ = reinterpret_cast<uint4*>(base + o);         o += al(sizeof(uint4) * (size_t)maxseg);
     c.plan = reinterpret_cast<uint2*>(base + o);         o += al(sizeof(uint2) * (size_t)maxseg);
     c.bflag = reinterpret_cast<uint32_t*>(base + o);     o += al(sizeof(uint32_t) * (size_t)n);
+    c.sflag = reinterpret_cast<uint32_t*>(base + o);     o += al(sizeof(uint32_t) * (size_t)maxseg);
+    c.incl = reinterpret_cast<uint4*>(base + o);         o += al(sizeof(uint4) * (size_t)maxseg);
+    c.ticket = reinterpret_cast<uint32_t*>(base + o);    o += al(sizeof(uint32_t));
     c.bytes = o;
     return c;
 }
@@ -575,6 +758,17 @@ inline uint32_t seg_grid(uint32_t maxseg, int ncu) {
     return g ? g : 1u;
 }
 inline uint32_t buf_grid(uint32_t n) { return (n + rle::kSegWaves - 1) / rle::kSegWaves; }
+// the fused single-pass encode (RLE_MI355X_SEG_FUSED=1; measured slower than the four launches, §4)
+#ifndef RLE_SEG_FUSED_DEFAULT
+#define RLE_SEG_FUSED_DEFAULT 0
+#endif
+bool seg_fused() {
+    static const bool on = [] {
+        const char* e = getenv("RLE_MI355X_SEG_FUSED");
+        return e ? e[0] != '0' : RLE_SEG_FUSED_DEFAULT != 0;
+    }();
+    return on;
+}
 }  // namespace
 
 extern "C" size_t rle_seg_workspace_bytes(uint32_t n, uint64_t total_in_bytes) {
@@ -599,7 +793,16 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
-    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first);
+    if (seg_fused()) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
+                           maxseg, w.ticket);
+        hipLaunchKernelGGL(rle::enc_seg_fused_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                           d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ,
+                           w.incl, w.sflag, w.ticket);
+        return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+    }
+    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
+                       nullptr);
     hipLaunchKernelGGL(rle::enc_seg_summary_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
                        d_in_off, d_in_len, n, w.seg_first, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::enc_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
@@ -625,7 +828,8 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
-    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first);
+    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
+                       nullptr);
     hipLaunchKernelGGL(rle::dec_seg_summary_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
                        d_in_off, d_in_len, n, w.seg_first, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::dec_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,

@@ -50,6 +50,8 @@ extern "C" {
 #define RLE_STATUS_SERIAL      0x100u  /* info: stream decoded by the exact serial path (not encoder output) */
 #define RLE_STATUS_SHORT       0x400u  /* info: the stream decodes to fewer than U bytes, the rest is zero
                                           (not encoder output) */
+#define RLE_STATUS_INTERNAL    0x800u  /* the segmented kernels' carry wait ran out (never expected): output
+                                          not trusted */
 
 /* Worst-case compressed size of U bytes (every run of length 2: 3 bytes per 2 input bytes). */
 size_t rle_max_compressed_size(size_t U);

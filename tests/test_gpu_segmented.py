@@ -102,3 +102,36 @@ def test_dropin_very_large_file():
     y = R.compress(x)
     assert y == O.encode(x)
     assert R.decompress(y, len(x)) == x
+
+
+_FUSED_CODE = r'''
+import sys
+sys.path[:0] = sys.argv[1:4]
+import rle_oracle as O
+from test_gpu_segmented import S
+from test_gpu_parity import gpu_encode
+xs = [bytes(3 * S + 5), O.gen(1, 1, 5 * S + 7), O.gen(2, 2, 2 * S), b"q" * (4 * S + 1), b"", b"a"]
+xs += [O.gen(k % 5, 40 + k, (k + 1) * 7000) for k in range(40)]
+xs.append(O.gen(3, 9, 64 << 20))   # one buffer of thousands of segments (the longest look-back)
+ys, st = gpu_encode(xs, seg=True)
+assert (st == 0).all(), st
+for i, x in enumerate(xs):
+    assert ys[i] == O.encode(x), (i, len(x))
+print("ok")
+'''
+
+
+def test_fused_single_pass_encode():
+    """The fused single-pass segmented encode (RLE_MI355X_SEG_FUSED=1, read at load: a fresh
+    process): ticket-ordered segments, write-through summaries and inclusive states, the decoupled
+    look-back, against the oracle -- including a 64 MiB buffer whose segments look back thousands
+    of places."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, RLE_MI355X_SEG_FUSED="1")
+    r = subprocess.run([sys.executable, "-c", _FUSED_CODE, os.path.join(root, "c-filestorage-server-and-client_amd"),
+                        os.path.join(root, "oracle"), here], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
