@@ -91,6 +91,9 @@ WORKLOADS = {
     "c4k_random": dict(n=4096, size=4096, kinds=(1,), ref_kinds="1", desc="4096 x 4 KiB random"),
     "c4k_zero": dict(n=4096, size=4096, kinds=(0,), ref_kinds="0", desc="4096 x 4 KiB zero"),
     "c4k_runs50": dict(n=4096, size=4096, kinds=(2,), ref_kinds="2", desc="4096 x 4 KiB runs50"),
+    # a quarter of a wave per SIMD (profiling with RLE_MI355X_COOP=0: one lone wave's walk)
+    "c4k_random_q": dict(n=256, size=4096, kinds=(1,), ref_kinds="1", desc="256 x 4 KiB random"),
+    "c4k_zero_q": dict(n=256, size=4096, kinds=(0,), ref_kinds="0", desc="256 x 4 KiB zero"),
     "s4k_mix": dict(n=65536, size=4096, kinds=(0, 1, 2, 3), ref_kinds="0,1,2,3", desc="65536 x 4 KiB zero/random/runs50/runs90"),
     "one4m": dict(n=1, size=4 << 20, kinds=(1,), ref_kinds="1", desc="1 x 4 MiB random (one large file)"),
     "one64m": dict(n=1, size=64 << 20, kinds=(2,), ref_kinds="2", desc="1 x 64 MiB runs50 (one large file)"),

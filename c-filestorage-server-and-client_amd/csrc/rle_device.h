@@ -1094,26 +1094,35 @@ __device__ __forceinline__ u32 enc_pair(const uint8_t* slotA, const uint8_t* slo
     const u32 r1 = enc_tile_an<true, kFast>(a1, lookB, pos1, U, U, lane, stage, dst, rso, st, kc, elut);
     return r0 + r1;
 }
-// The k64 walk two tiles per step (slots A, B; the last tile of an odd count alone, slot A).  As
-// walk_tiles: the wait before a step leaves only the previous step's stores in flight.
-template <class Pair, class Single>
-__device__ __forceinline__ void walk_pairs(u32x4 rs, u32 ntiles, u32 lane, const uint8_t* slots, Pair pair,
-                                           Single single) {
-    constexpr u32 kStride = kEncSlot;
-    const u32 lo = 16u * lane;
+// A walk two tiles per step (slots A, B; the last tile of an odd count alone, in slot A).  As
+// walk_tiles: the wait before a step leaves only the previous step's stores in flight; a step
+// returning ~0u stops the walk (drained; returns true).
+template <u32 kStep = kTileStep, bool kLook = false, class Pair, class Single>
+__device__ __forceinline__ bool walk_pairs(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots, Pair pair,
+                                           Single single, bool primed = false) {
+    constexpr u32 kStride = kLook ? kEncSlot : kSlot;
+    const u32 lo = start + 16u * lane;
     const u32 l0 = uniform(lds_addr(slots)), l1 = l0 + kStride;
-    const bool look = lane == 0u;
-    walk_prime<kEncStep, true>(rs, 0u, ntiles, lane, slots);
+    const bool look = kLook && lane == 0u;
+    if (!primed) walk_prime<kStep, kLook>(rs, start, ntiles, lane, slots);
     u32 p1 = 0, t = 0;
     for (; t + 1u < ntiles; t += 2u) {
         vm_wait(p1);
-        p1 = pair(t, slots, slots + kStride, Refill{rs, (t + 2u) * kEncStep + lo, l0, t + 2u < ntiles, look},
-                  Refill{rs, (t + 3u) * kEncStep + lo, l1, t + 3u < ntiles, look});
+        p1 = pair(t, slots, slots + kStride, Refill{rs, (t + 2u) * kStep + lo, l0, t + 2u < ntiles, look},
+                  Refill{rs, (t + 3u) * kStep + lo, l1, t + 3u < ntiles, look});
+        if (p1 == ~0u) {
+            vm_drain();
+            return true;
+        }
     }
     if (t < ntiles) {
         vm_wait(p1);
-        single(t, slots, Refill{rs, 0u, l0, false, look});
+        if (single(t, slots, Refill{rs, 0u, l0, false, look}) == ~0u) {
+            vm_drain();
+            return true;
+        }
     }
+    return false;
 }
 
 // ================================================================ DECODE
@@ -1692,14 +1701,12 @@ __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t*
 }
 
 // kChunks: the staging's chunks per wave (kDecChunks unless a kernel picks its own).
+// One tile from its preparation (dec_prepare): returns the store instructions issued, or ~0u (the
+// stream needs the exact serial path).
 template <bool kFast = false, u32 kChunks = kDecChunks>
-__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
-                                        u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
-                                        DecState& st, const DecK& kc, const u32x4* clut = nullptr) {
-    RLE_STAMP(st.sp, 0);   // DMA wait + loop
-    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
-    next();   // the slot is free once read
-    const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
+__device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
+                                           uint8_t* stage, uint8_t* dst, u32x4 rso, DecState& st, const DecK& kc,
+                                           const u32x4* clut) {
     // In a segment (Co < C) the literal path takes no tail tile: its tail form masks at the stream's
     // end, not at the segment's, and its last store may reach past the tile's output, which only a
     // later tile of the same wave rewrites (a segment's last tile is always a tail tile).
@@ -1789,6 +1796,16 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     st.prev = readlane(w[3], kOwnLanes - 1u);
     RLE_STAMP(st.sp, 7);   // partial-chunk move, state
     return rounds;
+}
+template <bool kFast = false, u32 kChunks = kDecChunks>
+__device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
+                                        u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
+                                        DecState& st, const DecK& kc, const u32x4* clut = nullptr) {
+    RLE_STAMP(st.sp, 0);   // DMA wait + loop
+    const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
+    next();   // the slot is free once read
+    const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
+    return dec_tile_pr<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
 }
 
 // After the last tile: outputs [flushed, end) = the partial chunk still staged (decoded positions

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     // 1024-byte tiles where they save a tile, up to kEncSmall (rle_device.h, enc_tile<true>)
     if (enc_ntiles_for(U) < ntiles_for(U) && U <= kEncSmall) {
         if (RLE_ENC_PAIR)   // two tiles per step (rle_device.h enc_pair)
-            walk_pairs(rsi, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
+            walk_pairs<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
                        [&](u32 t, const uint8_t* sa, const uint8_t* sb, const Refill& na, const Refill& nb) {
                            tl_mark(b, 2u + t, lane);
                            tl_mark(b, 3u + t, lane);

@@ -299,3 +299,47 @@ def test_periodic_tiles_decode_match_oracle():
         for i, y in enumerate(ys):
             ref, _ = O.decode(y, uu[i])
             assert dec[i] == ref, (delta, i)
+
+
+def test_encode_tile_pairs_match_oracle():
+    """Two encode tiles per step (csrc/rle_device.h enc_pair, buffers up to 16 KiB): every tile count
+    1..16 with the last tile 1..4 bytes, a few hundred, or full; pairs of run tiles (one run over
+    both, a boundary at the first byte, the run ending at, before and 1..9 bytes past the pair's
+    end), literal pairs (pairs of equal bytes straddling the two tiles and the pair's end, the
+    second tile the buffer's last with < 4, 4..16 and more output bytes), and every mix of run,
+    literal and general tiles within a pair; against the oracle."""
+    from test_gpu_parity import _oracle_parity
+    rng = np.random.default_rng(77)
+    xs = []
+    for nt in range(1, 17):
+        for last in (1, 2, 3, 4, 5, 300, 1023, 1024):
+            n = 1024 * (nt - 1) + last
+            for kind in (0, 1, 2, 3):
+                xs.append(O.gen(kind, 1000 * nt + last + kind, n))
+            xs.append(_pairs_data(rng, n, 0.06))
+    for k in (1, 2, 3, 6):   # pair boundaries at 2048 k
+        edge = 2048 * k
+        for back in range(0, 4):
+            for fwd in range(0, 11):
+                x = bytearray(_pairs_data(rng, edge + 600, 0.05))
+                # a run over the pair before the edge, ending fwd bytes past it
+                s0 = max(0, edge - 2048 - back)
+                x[s0:edge + fwd] = bytes([0x5A]) * (edge + fwd - s0)
+                if edge + fwd < len(x) and x[edge + fwd] == 0x5A:
+                    x[edge + fwd] = 0x5B
+                xs.append(bytes(x))
+                # a pair of equal bytes straddling the tiles' edges
+                y = bytearray(_pairs_data(rng, edge + 1024 + 3, 0.0))
+                for e in (edge - 1024, edge):
+                    if 1 <= e - back < len(y):
+                        y[e - back] = y[e - back - 1]
+                xs.append(bytes(y))
+    for i in range(200):   # run / literal / general tiles mixed inside pairs
+        n = int(rng.integers(1, 16385))
+        x = bytearray(_pairs_data(rng, n, float(rng.choice([0.0, 0.02, 0.2]))))
+        for _ in range(int(rng.integers(0, 4))):
+            a = int(rng.integers(0, n))
+            b = min(n, a + int(rng.integers(1, 3000)))
+            x[a:b] = bytes([int(rng.integers(0, 256))]) * (b - a)
+        xs.append(bytes(x))
+    _oracle_parity(xs)
