@@ -24,7 +24,15 @@ namespace rle {
 
 // Segment length: seg_tiles tiles of 1008 input bytes, a kernel argument chosen by the launcher
 // (4..64 tiles: about 16 segments per CU over the batch).
-constexpr u32 kSegTilesMin = 4, kSegTilesMax = 64;
+#ifndef RLE_SEG_TILES_MAX
+#define RLE_SEG_TILES_MAX 64
+#endif
+constexpr u32 kSegTilesMin = 4, kSegTilesMax = RLE_SEG_TILES_MAX;
+// decode write pass staging (chunks per wave, rle_device.h kDecChunks): fewer -> more waves per SIMD
+#ifndef RLE_SEG_DEC_CHUNKS
+#define RLE_SEG_DEC_CHUNKS RLE_DEC_CHUNKS
+#endif
+constexpr u32 kSegDecChunks = RLE_SEG_DEC_CHUNKS;
 constexpr u32 kSegWaves = 4;
 constexpr u32 kSegBlock = kWave * kSegWaves;
 constexpr u32 kNone = 0xFFFFFFFFu;
@@ -52,12 +60,16 @@ __device__ __forceinline__ u32 len32(uint64_t n) { return n > kMaxBufferBytes ? 
 // seg_first[i] = segments of buffers < i; seg_first[n] = total.  One workgroup.
 __global__ __launch_bounds__(1024) void seg_plan_kernel(const uint64_t* __restrict__ len, u32 n, u32 sb,
                                                         u32* __restrict__ seg_first, u32* __restrict__ sflag,
-                                                        u32 maxseg, u32* __restrict__ ticket) {
+                                                        u32 maxseg, u32* __restrict__ ticket,
+                                                        u32* __restrict__ bclear) {
     __shared__ u32 part[1024];
     const u32 t = threadIdx.x;
-    // (fused kernels) every segment's publication flag cleared, the ticket counter at 0
+    // (fused kernels) every segment's publication flag cleared, the ticket counter at 0, and (the
+    // single-pass decode) every buffer's flags
     if (sflag)
         for (u32 i = t; i < maxseg; i += 1024u) sflag[i] = 0u;
+    if (bclear)
+        for (u32 i = t; i < n; i += 1024u) bclear[i] = 0u;
     if (ticket && t == 0u) *ticket = 0u;
     const u32 per = (n + 1023u) / 1024u;
     const u32 b0 = t * per < n ? t * per : n;
@@ -91,6 +103,22 @@ __device__ __forceinline__ u32 seg_buffer(const u32* seg_first, u32 n, u32 g) {
     }
     return lo;
 }
+// seg_buf[g] = the buffer holding segment g, for every segment (one binary search per segment, all
+// in parallel), so the persistent summary and write waves find a segment's buffer with one load
+constexpr u32 kMapBlock = 256;
+__global__ __launch_bounds__(kMapBlock) void seg_map_kernel(const u32* __restrict__ seg_first, u32 n, u32 maxseg,
+                                                           u32* __restrict__ seg_buf) {
+    const u32 g = blockIdx.x * kMapBlock + threadIdx.x;
+    const u32 total = seg_first[n] < maxseg ? seg_first[n] : maxseg;
+    if (g >= total) return;
+    u32 lo = 0, hi = n;
+    while (hi - lo > 1u) {
+        const u32 mid = (lo + hi) >> 1;
+        if (seg_first[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    seg_buf[g] = lo;
+}
 __device__ __forceinline__ void seg_range(u32 i, u32 nseg, u32 n, u32 sb, u32& p0, u32& p1) {
     p0 = i * sb;
     p1 = (i + 1u == nseg) ? n : p0 + sb;
@@ -101,6 +129,42 @@ __device__ __forceinline__ u32 wave_sum(u32 x) { return readlane(wave_scan_incl(
 __device__ __forceinline__ u32 owned_sum(u32 x) { return readlane(wave_scan_incl(x, 0u, OpAdd()), kOwnLanes - 1u); }
 __device__ __forceinline__ bool owned_any(bool x) {
     return (__builtin_amdgcn_ballot_w64(x) & ((1ull << kOwnLanes) - 1ull)) != 0ull;
+}
+
+// A segment's tile walk: through the double-buffered LDS-DMA slots (walk_tiles), or (kRes) over a
+// segment already resident in LDS (res_load): tile t at mem + 1008 t, nothing to load or wait for.
+template <bool kRes, class Step>
+__device__ __forceinline__ bool walk_seg(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* mem, Step step) {
+    if (kRes) {
+#pragma clang loop unroll(disable)
+        for (u32 t = 0; t < ntiles; ++t)
+            if (step(t, mem + t * kTileStep, Refill{rs, 0u, 0u, false, false}) == ~0u) {
+                vm_drain();
+                return true;
+            }
+        return false;
+    }
+    return walk_tiles(rs, start, ntiles, lane, mem, step);
+}
+
+// Resident segments (the single-pass kernels below): a segment of at most kResTiles tiles is loaded
+// into the wave's LDS region once, [p0, p0 + 1008 nt + 16) in 1 KiB LDS-DMAs (range-checked: zeros
+// past the buffer), and both its summary and its output walk read it there.
+#ifndef RLE_RES_TILES
+#define RLE_RES_TILES 8
+#endif
+constexpr u32 kResTiles = RLE_RES_TILES;
+constexpr u32 kResBytes = (kResTiles * kTileStep + 16u + 1023u) & ~1023u;
+#ifndef RLE_RES_DEC_CHUNKS   // the resident decode's staging (chunks per wave; its region takes LDS too)
+#define RLE_RES_DEC_CHUNKS 96
+#endif
+constexpr u32 kResDecChunks = RLE_RES_DEC_CHUNKS;
+__device__ __forceinline__ void res_load(u32x4 rs, u32 p0, u32 nt, u32 lane, const uint8_t* region) {
+    const u32 l0 = uniform(lds_addr(region));
+    const u32 nd = uniform((nt * kTileStep + 16u + 1023u) >> 10);
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
+    for (u32 k = 0; k < nd; ++k) dma_tile<true>(rs, p0 + 1024u * k + 16u * lane, l0 + 1024u * k);
+    vm_drain();
 }
 
 // ================================================================ ENCODE
@@ -116,13 +180,14 @@ __device__ __forceinline__ u32 enc_piece_count(u32 L0, u32 q, u32 cont) {
 
 // One segment's encode summary (L0, lb + 1 or 0, rest, cont; see the top of this file): a walk over
 // its tiles, analysis only.  U > 0, src 16-byte aligned.
+template <bool kRes = false>
 __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u32 p0, u32 p1, u32 lane,
                                                    const uint8_t* slots) {
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     u32 prev_top = p0 ? (u32)src[p0 - 1u] << 24 : 0u;
     u32 rs = p0, fb = kNone, lb = kNone, rest = 0;
     const EncK kc = enc_k();
-    walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+    walk_seg<kRes>(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
         nx();
         const u32 pos = p0 + t * kTileStep;
@@ -177,7 +242,7 @@ __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u3
 __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_t* __restrict__ in,
                                                                     const uint64_t* __restrict__ in_off,
                                                                     const uint64_t* __restrict__ in_len, u32 n,
-                                                                    const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                    const u32* __restrict__ seg_first, const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                     uint4* __restrict__ summ) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
     const u32 lane = threadIdx.x & (kWave - 1);
@@ -186,7 +251,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
     for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
-        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 b = uniform(seg_buf[g]);
         const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
         const uint64_t U64 = in_len[b];
         const uint8_t* src = in + in_off[b];
@@ -266,6 +331,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_scan_kernel(const uint8_t* 
 }
 
 // One segment's output: the tile walk from its entering run start rs and output offset off.
+template <bool kRes = false>
 __device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, u32 U, u32 p0, u32 p1, u32 rs,
                                               u32 off, u32 lane, const uint8_t* slots, uint8_t* stage,
                                               const u32* elut) {
@@ -273,7 +339,7 @@ __device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, 
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
     EncState st{off, off & ~15u, p0 ? (u32)src[p0 - 1u] << 24 : 0u, rs, off & 15u, false, {}};
     const EncK kc = enc_k();
-    walk_tiles(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+    walk_seg<kRes>(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         // the fast tile paths (round 3; until then only the one-wave kernels took them): past the
         // segment's shared first chunk and before its last tile, as in a one-wave walk
         return enc_tile<false, RLE_SEG_FAST>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc, elut);
@@ -289,7 +355,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
                                                                   const uint64_t* __restrict__ in_len,
                                                                   uint8_t* __restrict__ out,
                                                                   const uint64_t* __restrict__ out_off, u32 n,
-                                                                  const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                  const u32* __restrict__ seg_first, const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                   const uint2* __restrict__ plan,
                                                                   const u32* __restrict__ bflag) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
@@ -305,7 +371,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
         const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
-        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 b = uniform(seg_buf[g]);
         if (uniform(bflag[b])) continue;
         const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
         const u32 U = (u32)in_len[b];
@@ -461,6 +527,99 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
     }
 }
 
+
+// ---------------------------------------------------------------- resident single-pass encode
+// SURVEY.md §5's single pass, with the segment held in LDS: a wave takes kResTicket consecutive
+// segments per ticket (one global atomic per ticket, not per segment: a single counter serialises
+// its atomics, ~12-16 ns each, r3s), and for each segment loads its <= kResTiles tiles into its LDS
+// region once, summarises them there, publishes the summary, derives its entering state with the
+// decoupled look-back of the fused kernel above, publishes its inclusive state and walks the same
+// LDS tiles again to write.  HBM sees the input once.  Progress: as in the fused kernel, a wave
+// waits only on segments of earlier tickets, whose waves are running.
+#ifndef RLE_RES_TICKET
+#define RLE_RES_TICKET 4
+#endif
+constexpr u32 kResTicket = RLE_RES_TICKET;
+__global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ in_off,
+                                                                const uint64_t* __restrict__ in_len,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                uint64_t* __restrict__ out_len,
+                                                                uint32_t* __restrict__ status, u32 n,
+                                                                const u32* __restrict__ seg_first,
+                                                                const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
+                                                                uint4* __restrict__ summ, uint4* __restrict__ incl,
+                                                                u32* __restrict__ sflag, u32* __restrict__ ticket) {
+    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kEncStage];
+    __shared__ __attribute__((aligned(16))) u32 elut[kInsWaveWords];   // enc_tile_fast's selectors
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    uint8_t* stage = stage_all + wid * kEncStage;
+    const uint8_t* region = region_all + wid * kResBytes;
+    for (u32 k = threadIdx.x; k < kInsWaveWords; k += kSegBlock) elut[k] = kEncInsLut.s[k];
+    __syncthreads();
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (;;) {
+        u32 g0 = 0;
+        if (lane == 0) g0 = atomicAdd(ticket, kResTicket);
+        g0 = uniform(g0);
+        if (g0 >= total) break;
+        const u32 g1 = g0 + kResTicket < total ? g0 + kResTicket : total;
+        for (u32 g = g0; g < g1; ++g) {
+            const u32 b = uniform(seg_buf[g]);
+            const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
+            const uint64_t U64 = in_len[b];
+            const uint8_t* src = in + in_off[b];
+            uint8_t* dst = out + out_off[b];
+            u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+            if (U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
+            if (bad || U64 == 0u) {   // the buffer's segments all skip (an empty buffer is one segment)
+                if (g == s0 && lane == 0) {
+                    out_len[b] = 0;
+                    if (status) status[b] = bad;
+                }
+                continue;
+            }
+            const u32 U = (u32)U64;
+            u32 p0, p1;
+            seg_range(g - s0, nseg, U, sb, p0, p1);
+            res_load(make_rsrc(src, (U + 15u) & ~15u), p0, ntiles_for(p1 - p0), lane, region);
+            const uint4 sm = enc_seg_summarize<true>(src, U, p0, p1, lane, region);
+            if (lane == 0) publish(summ + g, sm, sflag + g, kFlagAgg);
+            bool late = false;
+            EncCarry c{0u, 0u};
+            u32 lateb = 0u;
+            if (g > s0) {
+                const u32 from = seg_lookback(g, s0, sflag, lane, late);
+                if (from > s0) {
+                    const uint4 in4 = ld_relaxed4(incl + (from - 1u));
+                    c = EncCarry{uniform(in4.x), uniform(in4.y)};
+                    lateb = uniform(in4.z);
+                }
+                for (u32 base = from; base < g; base += kWave) {
+                    const u32 j = base + lane;
+                    const bool valid = j < g;
+                    const uint4 smj = valid ? ld_relaxed4(summ + j) : make_uint4(0u, 0u, 0u, 0u);
+                    enc_seg_window(smj, valid, (j - s0) * sb, c);
+                }
+            }
+            const uint2 mine = enc_seg_window(sm, lane == 0u, p0, c);
+            lateb |= late ? RLE_STATUS_INTERNAL : 0u;
+            if (lane == 0) {
+                publish(incl + g, make_uint4(c.lb1, c.off, lateb, 0u), sflag + g, kFlagIncl);
+                if (g + 1u == s1) {   // the buffer's last segment: C and the status
+                    out_len[b] = c.off;
+                    if (status) status[b] = lateb ? lateb : RLE_STATUS_OK;
+                }
+            }
+            enc_seg_write<true>(src, dst, U, p0, p1, uniform(mine.x), uniform(mine.y), lane, region, stage, elut);
+        }
+    }
+}
+
 // ================================================================ DECODE
 // Decoded bytes of a non-tail tile entered at phase d when every pair token in it is "v v 2" (random
 // and text-like data): then each token's output is its own bytes with the count digit deleted, so
@@ -498,10 +657,55 @@ __device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 l
     return wave_sum((u32)__builtin_popcount(K));
 }
 
+// One segment's decode summary: for each entry phase 0..2, the decoded bytes (.x .y .z) and, in .w,
+// the exit phases (2 bits each) and the phases whose tiled path declines (bits 8..10).  C > 0.
+template <bool kRes = false>
+__device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u32 q0, u32 q1, u32 lane,
+                                                   const uint8_t* slots, const DecEntry* tbl) {
+    const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+    u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
+    const DecK kc = dec_k();
+    walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
+        nx();
+        const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
+        const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
+        if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
+            u32 tot = (RLE_SEG_SUMFAST && !pr.tail) ? dec_count_literal(pr, d0, lane, kc) : kNotFast;
+            bool bad = false;
+            if (tot == kNotFast) {
+                const DecLen ln = dec_lengths(pr, d0);
+                tot = owned_sum(ln.nout);
+                bad = owned_any(ln.serial_lane);
+            }
+            c0 += tot; c1 += tot; c2 += tot;
+            badm |= bad ? 7u : 0u;
+            d0 = d1 = d2 = bfe(m63, 8u * d0, 8);
+        } else {
+            const DecLen l0 = dec_lengths(pr, d0);
+            c0 += owned_sum(l0.nout);
+            badm |= owned_any(l0.serial_lane) ? 1u : 0u;
+            const DecLen l1 = dec_lengths(pr, d1);
+            c1 += owned_sum(l1.nout);
+            badm |= owned_any(l1.serial_lane) ? 2u : 0u;
+            const DecLen l2 = dec_lengths(pr, d2);
+            c2 += owned_sum(l2.nout);
+            badm |= owned_any(l2.serial_lane) ? 4u : 0u;
+            d0 = bfe(m63, 8u * d0, 8);
+            d1 = bfe(m63, 8u * d1, 8);
+            d2 = bfe(m63, 8u * d2, 8);
+        }
+        return 0u;
+    });
+    return make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8));
+}
+// the summary of an empty stream: counts 0, exit = entry
+constexpr uint4 kDecEmpty = {0u, 0u, 0u, 0u | (1u << 2) | (2u << 4)};
+
 __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_t* __restrict__ in,
                                                                     const uint64_t* __restrict__ in_off,
                                                                     const uint64_t* __restrict__ in_len, u32 n,
-                                                                    const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                    const u32* __restrict__ seg_first, const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                     uint4* __restrict__ summ) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
     __shared__ DecEntry tbl[256];
@@ -513,54 +717,42 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
     for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
-        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 b = uniform(seg_buf[g]);
         const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
         const uint64_t C64 = in_len[b];
         const uint8_t* src = in + in_off[b];
-        uint4 res = make_uint4(0u, 0u, 0u, 0u | (1u << 2) | (2u << 4));   // empty: counts 0, exit = entry
+        uint4 res = kDecEmpty;
         if (C64 > 0 && C64 <= kMaxBufferBytes && !((uintptr_t)src & 15u)) {
-            const u32 C = (u32)C64;
             u32 q0, q1;
-            seg_range(g - s0, nseg, C, sb, q0, q1);
-            const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
-            u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
-            const DecK kc = dec_k();
-            walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
-                nx();
-                const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
-                const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
-                if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
-                    u32 tot = (RLE_SEG_SUMFAST && !pr.tail) ? dec_count_literal(pr, d0, lane, kc) : kNotFast;
-                    bool bad = false;
-                    if (tot == kNotFast) {
-                        const DecLen ln = dec_lengths(pr, d0);
-                        tot = owned_sum(ln.nout);
-                        bad = owned_any(ln.serial_lane);
-                    }
-                    c0 += tot; c1 += tot; c2 += tot;
-                    badm |= bad ? 7u : 0u;
-                    d0 = d1 = d2 = bfe(m63, 8u * d0, 8);
-                } else {
-                    const DecLen l0 = dec_lengths(pr, d0);
-                    c0 += owned_sum(l0.nout);
-                    badm |= owned_any(l0.serial_lane) ? 1u : 0u;
-                    const DecLen l1 = dec_lengths(pr, d1);
-                    c1 += owned_sum(l1.nout);
-                    badm |= owned_any(l1.serial_lane) ? 2u : 0u;
-                    const DecLen l2 = dec_lengths(pr, d2);
-                    c2 += owned_sum(l2.nout);
-                    badm |= owned_any(l2.serial_lane) ? 4u : 0u;
-                    d0 = bfe(m63, 8u * d0, 8);
-                    d1 = bfe(m63, 8u * d1, 8);
-                    d2 = bfe(m63, 8u * d2, 8);
-                }
-                return 0u;
-            });
-            res = make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8));
+            seg_range(g - s0, nseg, (u32)C64, sb, q0, q1);
+            res = dec_seg_summarize(src, (u32)C64, q0, q1, lane, slots, tbl);
         }
         if (lane == 0) summ[g] = res;
     }
+}
+
+// The carried state of a decode scan over a buffer's segments: the entry phase, the output offset
+// and whether the buffer needs the exact serial path (a taken phase declines, or the stream decodes
+// past U).  One window of up to 64 consecutive segments (lane i: segment base + i, summary sm); each
+// lane gets its segment's entry phase and output offset; c advances past the window.  Shared by the
+// per-buffer scan and the single-pass kernel's look-back.
+struct DecCarry {
+    u32 e, off;
+    bool serial;
+};
+__device__ __forceinline__ uint2 dec_seg_window(uint4 sm, bool valid, u32 U, DecCarry& c) {
+    const u32 sel = valid ? (bfe(sm.w, 0, 2) | (bfe(sm.w, 2, 2) << 8) | (bfe(sm.w, 4, 2) << 16) | (3u << 24)) : kMapId;
+    const u32 incl = wave_scan_incl(sel, kMapId, OpMap());
+    const u32 e = bfe(from_prev_lane(incl, kMapId), 8u * c.e, 8);
+    const u32 cnt = valid ? (e == 0u ? sm.x : (e == 1u ? sm.y : sm.z)) : 0u;
+    c.serial |= __builtin_amdgcn_ballot_w64(valid && ((sm.w >> (8u + e)) & 1u)) != 0;
+    const u32 oincl = wave_scan_incl(cnt, 0u, OpAdd());
+    const uint2 r = make_uint2(e, c.off + oincl - cnt);
+    c.e = bfe(readlane(incl, 63), 8u * c.e, 8);
+    const u32 add = readlane(oincl, 63);
+    if (add > U - (c.off < U ? c.off : U)) c.serial = true;   // decodes past U
+    c.off += add;
+    return r;
 }
 
 // one wave per buffer: entry phase and output offset of every segment; serial when the taken
@@ -594,25 +786,35 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_scan_kernel(const uint8_t* 
         return;
     }
     const u32 U = (u32)U64;
-    u32 e_carry = 0, carry_off = 0;
-    bool serial = false;
+    DecCarry c{0u, 0u, false};
     for (u32 base = s0; base < s1; base += kWave) {
         const u32 g = base + lane;
         const bool valid = g < s1;
         const uint4 sm = valid ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
-        const u32 sel = valid ? (bfe(sm.w, 0, 2) | (bfe(sm.w, 2, 2) << 8) | (bfe(sm.w, 4, 2) << 16) | (3u << 24)) : kMapId;
-        const u32 incl = wave_scan_incl(sel, kMapId, OpMap());
-        const u32 e = bfe(from_prev_lane(incl, kMapId), 8u * e_carry, 8);
-        const u32 cnt = valid ? (e == 0u ? sm.x : (e == 1u ? sm.y : sm.z)) : 0u;
-        serial |= __builtin_amdgcn_ballot_w64(valid && ((sm.w >> (8u + e)) & 1u)) != 0;
-        const u32 oincl = wave_scan_incl(cnt, 0u, OpAdd());
-        if (valid) plan[g] = make_uint2(e, carry_off + oincl - cnt);
-        e_carry = bfe(readlane(incl, 63), 8u * e_carry, 8);
-        const u32 add = readlane(oincl, 63);
-        if (add > U - (carry_off < U ? carry_off : U)) serial = true;   // decodes past U
-        carry_off += add;
+        const uint2 pl = dec_seg_window(sm, valid, U, c);
+        if (valid) plan[g] = pl;
     }
-    if (lane == 0) bflag[b] = serial ? kFlagSerial : 0u;
+    if (lane == 0) bflag[b] = c.serial ? kFlagSerial : 0u;
+}
+
+// One segment's output: the tile walk from entry phase e and output offset off; the stream's last
+// segment (last) also writes the bytes up to U and the status (st_b, when given).
+template <bool kRes, u32 kChunks>
+__device__ __forceinline__ void dec_seg_write(const uint8_t* src, uint8_t* dst, u32 C, u32 U, u32 q0, u32 q1, u32 e,
+                                              u32 off, bool last, u32 lane, const uint8_t* slots, uint8_t* stage,
+                                              const DecEntry* tbl, const u32x4* clut, uint32_t* st_b) {
+    const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U);
+    DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, false, {}};
+    const DecK kc = dec_k();
+    const bool serial = walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        // the fast tile paths (round 3): past the segment's shared first chunk, and the literal
+        // path only on tiles a later tile of this segment follows (dec_tile)
+        return dec_tile<RLE_SEG_FAST, kChunks>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc,
+                                               clut);
+    });
+    dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
+    if (last && lane == 0 && st_b) *st_b = serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : dec_tiled_status(st, U);
 }
 
 __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t* __restrict__ in,
@@ -623,11 +825,12 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
                                                                   const uint64_t* __restrict__ out_len,
                                                                   const uint64_t* __restrict__ out_cap,
                                                                   uint32_t* __restrict__ status, u32 n,
-                                                                  const u32* __restrict__ seg_first, u32 maxseg, u32 sb,
+                                                                  const u32* __restrict__ seg_first, const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                   const uint2* __restrict__ plan,
                                                                   const u32* __restrict__ bflag) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
-    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kDecStage];
+    constexpr u32 kStage = 32u * kSegDecChunks;
+    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kStage];
     __shared__ DecEntry tbl[256];
     __shared__ u32x4 clut[kCompactEntries];   // dec_tile_fast's selectors
     const u32 lane = threadIdx.x & (kWave - 1);
@@ -636,16 +839,16 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
     for (u32 k = threadIdx.x; k < kCompactEntries; k += kSegBlock)
         clut[k] = u32x4{kCompactLut.s[4u * k], kCompactLut.s[4u * k + 1u], kCompactLut.s[4u * k + 2u],
                         kCompactLut.s[4u * k + 3u]};
-    uint8_t* stage = stage_all + wid * kDecStage;
+    uint8_t* stage = stage_all + wid * kStage;
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    for (u32 k = lane; k < kDecStage / 16u; k += kWave)
+    for (u32 k = lane; k < kStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
         const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
-        const u32 b = seg_buffer(seg_first, n, g);
+        const u32 b = uniform(seg_buf[g]);
         const u32 flag = uniform(bflag[b]);
         if (flag & kFlagSkip) continue;
         const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
@@ -655,7 +858,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         if (flag & kFlagSerial) {   // one wave decodes the whole buffer exactly
             if (g == s0) {
                 const uint64_t cap = out_cap ? out_cap[b] : (uint64_t)U;
-                const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage);
+                const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage, kStage);
                 if (lane == 0 && status) status[b] = stat;
             }
             continue;
@@ -663,20 +866,128 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         u32 q0, q1;
         seg_range(g - s0, nseg, C, sb, q0, q1);
         const uint2 pl = plan[g];
-        const u32 e = uniform(pl.x), off = uniform(pl.y);
-        const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
-        const u32x4 rso = make_rsrc(dst, U);
-        DecState st{off, off & ~15u, e, 0u, 0u, off & 15u, 0u, false, {}};
-        const DecK kc = dec_k();
-        const bool serial = walk_tiles(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
-            // the fast tile paths (round 3): past the segment's shared first chunk, and the literal
-            // path only on tiles a later tile of this segment follows (dec_tile)
-            return dec_tile<RLE_SEG_FAST>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc, clut);
-        });
-        const bool last = g + 1u == s0 + nseg;
-        dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
-        if (last && lane == 0 && status) status[b] = serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : dec_tiled_status(st, U);
+        dec_seg_write<false, kSegDecChunks>(src, dst, C, U, q0, q1, uniform(pl.x), uniform(pl.y), g + 1u == s0 + nseg,
+                                            lane, slots, stage, tbl, clut, status ? status + b : nullptr);
     }
+}
+
+
+// ---------------------------------------------------------------- resident single-pass decode
+// The decode form of enc_seg_res_kernel: a segment's summary is its three entry phases' counts and
+// exits (dec_seg_summarize), its entering phase and offset come from the look-back (dec_seg_window
+// over the published summaries), and its output walk reads the same LDS tiles.  A buffer that needs
+// the exact serial path (a taken phase declines, the stream decodes past U, or a look-back ran out
+// of polls) is only known once its last segment has combined: its segments skip their walks from
+// the first one that knows, the buffer is flagged (bflag, cleared by the plan), and
+// dec_seg_serial_kernel decodes it after this launch, over whatever the earlier segments wrote.
+__global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ in_off,
+                                                                const uint64_t* __restrict__ in_len,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_len,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint32_t* __restrict__ status, u32 n,
+                                                                const u32* __restrict__ seg_first,
+                                                                const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
+                                                                uint4* __restrict__ summ, uint4* __restrict__ incl,
+                                                                u32* __restrict__ sflag, u32* __restrict__ ticket,
+                                                                u32* __restrict__ bflag) {
+    constexpr u32 kStage = 32u * kResDecChunks;
+    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResBytes];
+    __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kStage];
+    __shared__ DecEntry tbl[256];
+    __shared__ u32x4 clut[kCompactEntries];   // dec_tile_fast's selectors
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    for (u32 k = threadIdx.x; k < 256u; k += kSegBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
+    for (u32 k = threadIdx.x; k < kCompactEntries; k += kSegBlock)
+        clut[k] = u32x4{kCompactLut.s[4u * k], kCompactLut.s[4u * k + 1u], kCompactLut.s[4u * k + 2u],
+                        kCompactLut.s[4u * k + 3u]};
+    uint8_t* stage = stage_all + wid * kStage;
+    const uint8_t* region = region_all + wid * kResBytes;
+    for (u32 k = lane; k < kStage / 16u; k += kWave) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    u32 total = uniform(seg_first[n]);
+    total = total < maxseg ? total : maxseg;
+    for (;;) {
+        u32 g0 = 0;
+        if (lane == 0) g0 = atomicAdd(ticket, kResTicket);
+        g0 = uniform(g0);
+        if (g0 >= total) break;
+        const u32 g1 = g0 + kResTicket < total ? g0 + kResTicket : total;
+        for (u32 g = g0; g < g1; ++g) {
+            const u32 b = uniform(seg_buf[g]);
+            const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
+            const uint64_t C64 = in_len[b], U64 = out_len[b];
+            const uint64_t cap = out_cap ? out_cap[b] : U64;
+            const uint8_t* src = in + in_off[b];
+            uint8_t* dst = out + out_off[b];
+            u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
+            if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
+            if (bad) {   // the buffer's segments all skip
+                if (g == s0 && lane == 0 && status) status[b] = bad;
+                continue;
+            }
+            const u32 C = (u32)C64, U = (u32)U64;
+            u32 q0, q1;
+            seg_range(g - s0, nseg, C, sb, q0, q1);
+            uint4 sm = kDecEmpty;
+            if (C) {
+                res_load(make_rsrc(src, (C + 15u) & ~15u), q0, ntiles_for(q1 - q0), lane, region);
+                sm = dec_seg_summarize<true>(src, C, q0, q1, lane, region, tbl);
+            }
+            if (lane == 0) publish(summ + g, sm, sflag + g, kFlagAgg);
+            bool late = false;
+            DecCarry c{0u, 0u, false};
+            if (g > s0) {
+                const u32 from = seg_lookback(g, s0, sflag, lane, late);
+                if (from > s0) {
+                    const uint4 in4 = ld_relaxed4(incl + (from - 1u));
+                    c = DecCarry{uniform(in4.x), uniform(in4.y), uniform(in4.z) != 0u};
+                }
+                for (u32 base = from; base < g; base += kWave) {
+                    const u32 j = base + lane;
+                    const bool valid = j < g;
+                    const uint4 smj = valid ? ld_relaxed4(summ + j) : make_uint4(0u, 0u, 0u, 0u);
+                    dec_seg_window(smj, valid, U, c);
+                }
+            }
+            const uint2 mine = dec_seg_window(sm, lane == 0u, U, c);
+            c.serial = c.serial || late;
+            const bool last = g + 1u == s1;
+            if (lane == 0) {
+                publish(incl + g, make_uint4(c.e, c.off, c.serial ? 1u : 0u, 0u), sflag + g, kFlagIncl);
+                // the buffer's serial flag: from its last segment, or from any segment whose
+                // look-back ran out (its state may not reach the last segment's combine)
+                if ((last && c.serial) || late) atomicOr(bflag + b, kFlagSerial);
+            }
+            if (!c.serial)
+                dec_seg_write<true, kResDecChunks>(src, dst, C, U, q0, q1, uniform(mine.x), uniform(mine.y), last, lane,
+                                                   region, stage, tbl, clut, status ? status + b : nullptr);
+        }
+    }
+}
+
+// After dec_seg_res_kernel: the exact serial decode of the buffers it flagged, one wave each.
+__global__ __launch_bounds__(kSegBlock) void dec_seg_serial_kernel(const uint8_t* __restrict__ in,
+                                                                   const uint64_t* __restrict__ in_off,
+                                                                   const uint64_t* __restrict__ in_len,
+                                                                   uint8_t* __restrict__ out,
+                                                                   const uint64_t* __restrict__ out_off,
+                                                                   const uint64_t* __restrict__ out_len,
+                                                                   const uint64_t* __restrict__ out_cap,
+                                                                   uint32_t* __restrict__ status, u32 n,
+                                                                   const u32* __restrict__ bflag) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * 1024];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    const u32 b = blockIdx.x * kSegWaves + wid;
+    if (b >= n || !(uniform(bflag[b]) & kFlagSerial)) return;
+    const u32 U = (u32)out_len[b];
+    const uint64_t cap = out_cap ? out_cap[b] : (uint64_t)U;
+    const u32 stat = dec_serial(in + in_off[b], (u32)in_len[b], U, cap, out + out_off[b], lane, stage_all + wid * 1024, 1024);
+    if (lane == 0 && status) status[b] = stat;
 }
 
 }  // namespace rle
@@ -701,6 +1012,7 @@ CuCache& cu_cache() {
 // 256 B-aligned carve-up of the workspace
 struct Carve {
     uint32_t* seg_first;
+    uint32_t* seg_buf;   // per-segment buffer index (seg_map_kernel)
     uint4* summ;
     uint2* plan;
     uint32_t* bflag;
@@ -714,6 +1026,7 @@ Carve carve(char* base, uint32_t n, uint32_t maxseg) {
     Carve c;
     size_t o = 0;
     c.seg_first = reinterpret_cast<uint32_t*>(base + o); o += al(sizeof(uint32_t) * ((size_t)n + 1));
+    c.seg_buf = reinterpret_cast<uint32_t*>(base + o);   o += al(sizeof(uint32_t) * (size_t)maxseg);
     c.summ = reinterpret_cast<uint4*>(base + o);         o += al(sizeof(uint4) * (size_t)maxseg);
     c.plan = reinterpret_cast<uint2*>(base + o);         o += al(sizeof(uint2) * (size_t)maxseg);
     c.bflag = reinterpret_cast<uint32_t*>(base + o);     o += al(sizeof(uint32_t) * (size_t)n);
@@ -744,19 +1057,43 @@ int device_cus(int* ncu) {
     return RLE_OK;
 }
 // segment length in bytes: about 16 segments per CU over the batch, 4..64 tiles each
+// (RLE_SEG_TILES_FIX > 0: a fixed segment length, for A/B builds)
+#ifndef RLE_SEG_TILES_FIX
+#define RLE_SEG_TILES_FIX 0
+#endif
+// The resident single-pass kernels (enc_seg_res_kernel / dec_seg_res_kernel): RLE_MI355X_SEG_RES=1|0
+// overrides the build default.  Their segments are one LDS region's tiles, 16 bytes short, so that a
+// buffer's last segment (which absorbs a remainder of up to 2 bytes) still fits.
+#ifndef RLE_SEG_RES_DEFAULT
+#define RLE_SEG_RES_DEFAULT 0
+#endif
+bool seg_res() {
+    static const bool on = [] {
+        const char* e = getenv("RLE_MI355X_SEG_RES");
+        return e ? e[0] != '0' : RLE_SEG_RES_DEFAULT != 0;
+    }();
+    return on;
+}
 inline uint32_t seg_bytes(uint64_t total, int ncu) {
+    if (seg_res()) return rle::kResTiles * rle::kTileStep - 16u;
+    if (RLE_SEG_TILES_FIX) return (uint32_t)RLE_SEG_TILES_FIX * rle::kTileStep;
     const uint64_t tiles = (total + rle::kTileStep - 1) / rle::kTileStep;
     uint64_t per = tiles / ((uint64_t)ncu * 16u);
     per = per < rle::kSegTilesMin ? rle::kSegTilesMin : (per > rle::kSegTilesMax ? rle::kSegTilesMax : per);
     return (uint32_t)per * rle::kTileStep;
 }
-// persistent grids: enough workgroups to fill every CU (4 per CU), never more than the segments
+// persistent grids: enough workgroups to fill every CU (RLE_SEG_OCC per CU), never more than the
+// segments
+#ifndef RLE_SEG_OCC
+#define RLE_SEG_OCC 4
+#endif
 inline uint32_t seg_grid(uint32_t maxseg, int ncu) {
     const uint32_t need = (maxseg + rle::kSegWaves - 1) / rle::kSegWaves;
-    const uint32_t fill = (uint32_t)ncu * 4u;
+    const uint32_t fill = (uint32_t)ncu * RLE_SEG_OCC;
     const uint32_t g = need < fill ? need : fill;
     return g ? g : 1u;
 }
+inline uint32_t map_grid(uint32_t maxseg) { return (maxseg + rle::kMapBlock - 1) / rle::kMapBlock; }
 inline uint32_t buf_grid(uint32_t n) { return (n + rle::kSegWaves - 1) / rle::kSegWaves; }
 // the fused single-pass encode (RLE_MI355X_SEG_FUSED=1; measured slower than the four launches, §4)
 #ifndef RLE_SEG_FUSED_DEFAULT
@@ -793,22 +1130,35 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
+    if (seg_res()) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
+                           maxseg, w.ticket, nullptr);
+        hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
+                           maxseg, w.seg_buf);
+        hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                           d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, w.seg_buf, maxseg,
+                           sb, w.summ, w.incl, w.sflag, w.ticket);
+        return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+    }
     if (seg_fused()) {
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
-                           maxseg, w.ticket);
+                           maxseg, w.ticket, nullptr);
         hipLaunchKernelGGL(rle::enc_seg_fused_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ,
                            w.incl, w.sflag, w.ticket);
         return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
     }
+    const uint32_t grid = seg_grid(maxseg, ncu);
     hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
-                       nullptr);
-    hipLaunchKernelGGL(rle::enc_seg_summary_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
-                       d_in_off, d_in_len, n, w.seg_first, maxseg, sb, w.summ);
+                       nullptr, nullptr);
+    hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n, maxseg,
+                       w.seg_buf);
+    hipLaunchKernelGGL(rle::enc_seg_summary_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, n,
+                       w.seg_first, w.seg_buf, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::enc_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
                        out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
-    hipLaunchKernelGGL(rle::enc_seg_write_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
-                       d_in_off, d_in_len, out, d_out_off, n, w.seg_first, maxseg, sb, w.plan, w.bflag);
+    hipLaunchKernelGGL(rle::enc_seg_write_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out,
+                       d_out_off, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 
@@ -828,14 +1178,28 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
+    if (seg_res()) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
+                           maxseg, w.ticket, w.bflag);
+        hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
+                           maxseg, w.seg_buf);
+        hipLaunchKernelGGL(rle::dec_seg_res_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+                           d_in_off, d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first,
+                           w.seg_buf, maxseg, sb, w.summ, w.incl, w.sflag, w.ticket, w.bflag);
+        hipLaunchKernelGGL(rle::dec_seg_serial_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off,
+                           d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.bflag);
+        return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+    }
+    const uint32_t grid = seg_grid(maxseg, ncu);
     hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
-                       nullptr);
-    hipLaunchKernelGGL(rle::dec_seg_summary_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
-                       d_in_off, d_in_len, n, w.seg_first, maxseg, sb, w.summ);
+                       nullptr, nullptr);
+    hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n, maxseg,
+                       w.seg_buf);
+    hipLaunchKernelGGL(rle::dec_seg_summary_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, n,
+                       w.seg_first, w.seg_buf, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::dec_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
                        out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
-    hipLaunchKernelGGL(rle::dec_seg_write_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
-                       d_in_off, d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, maxseg, sb,
-                       w.plan, w.bflag);
+    hipLaunchKernelGGL(rle::dec_seg_write_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out,
+                       d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }

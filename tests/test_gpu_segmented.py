@@ -4,6 +4,8 @@ the cases sit on and around segment edges, carry runs and token phases across th
 '9' runs, whose decode phases never re-synchronise), mix buffer sizes, and feed invalid streams
 that must fall back to the exact serial decoder.  The algebra itself is pinned on CPU by
 tests/test_seg_model.py."""
+import os
+
 import numpy as np
 import pytest
 
@@ -12,7 +14,11 @@ import rle_oracle as O
 from test_gpu_parity import gpu_decode, gpu_encode
 
 pytestmark = pytest.mark.gpu
-S = 64512
+# segment length of the path under test: 64512 for the four-launch kernels at these batch sizes;
+# 8048 (8 tiles less 16 bytes) for the resident single-pass kernels (RLE_MI355X_SEG_RES=1, which
+# test_resident_single_pass below sets for a second run of this module)
+RES = os.environ.get("RLE_MI355X_SEG_RES", "0") == "1"
+S = 8048 if RES else 64512
 
 
 def _parity(xs):
@@ -135,3 +141,19 @@ def test_fused_single_pass_encode():
     r = subprocess.run([sys.executable, "-c", _FUSED_CODE, os.path.join(root, "c-filestorage-server-and-client_amd"),
                         os.path.join(root, "oracle"), here], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+
+
+def test_resident_single_pass():
+    """The resident single-pass segmented kernels (RLE_MI355X_SEG_RES=1, read at load: a fresh
+    process): this whole module again, with its segment edges at the resident segment length, plus
+    the drop-in's large files, against the oracle."""
+    if RES:
+        pytest.skip("already the resident run")
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, RLE_MI355X_SEG_RES="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(here, "test_gpu_segmented.py"), "-k", "not fused and not resident"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])

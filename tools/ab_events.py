@@ -28,6 +28,8 @@ def load(path):
     sz = ctypes.c_size_t
     L.rle_encode_batch_device_seg.argtypes = [vp] * 7 + [u32, u64, vp, sz, vp]
     L.rle_decode_batch_device_seg.argtypes = [vp] * 8 + [u32, u64, vp, sz, vp]
+    L.rle_seg_workspace_bytes.argtypes = [u32, u64]
+    L.rle_seg_workspace_bytes.restype = sz
     return L
 
 
@@ -51,17 +53,25 @@ def main():
         B = bench.Batch(bench.WORKLOADS[wl], 0, 1, dev)
         B.encode(s)
         B.calibrate()
-        ref_c = B.d_c.clone()
+        ref_clen = B.clens[0].clone()
         clen = B.clens[0]
 
-        we, wd = B.ws_enc, B.ws_dec
+        # each build sizes its own segmented workspace (builds may cut segments differently)
+        wse, wsd = {}, {}
+        for k, L in libs.items():
+            wse[k] = torch.empty(int(L.rle_seg_workspace_bytes(B.n, B.u_bytes)) + 256, dtype=torch.uint8, device=dev)
+            wsd[k] = torch.empty(int(L.rle_seg_workspace_bytes(B.n, B.c_cap)) + 256, dtype=torch.uint8, device=dev)
         al = lambda w: ctypes.c_void_p((w.data_ptr() + 255) & ~255)
         wn = lambda w: w.numel() - 256
+        name = {id(L): k for k, L in libs.items()}
+        inmask = torch.zeros(B.d_in.numel(), dtype=torch.bool, device=dev)
+        for o, u in zip(B.offs.tolist(), B.lens.tolist()):
+            inmask[o:o + u] = True
 
         def enc(L):
             if a.seg:
                 L.rle_encode_batch_device_seg(P(B.d_in), P(B.offs), P(B.lens), P(B.d_c), P(B.coffs), P(clen),
-                                              P(B.status), B.n, B.u_bytes, al(we), wn(we), sp)
+                                              P(B.status), B.n, B.u_bytes, al(wse[name[id(L)]]), wn(wse[name[id(L)]]), sp)
             else:
                 L.rle_encode_batch_device_sized(P(B.d_in), P(B.offs), P(B.lens), P(B.d_c), P(B.coffs), P(clen),
                                                 P(B.status), B.n, B.max_u, sp)
@@ -69,18 +79,20 @@ def main():
         def dec(L):
             if a.seg:
                 L.rle_decode_batch_device_seg(P(B.d_c), P(B.coffs), P(clen), P(B.d_out), P(B.offs), P(B.lens), None,
-                                              P(B.status), B.n, B.c_cap, al(wd), wn(wd), sp)
+                                              P(B.status), B.n, B.c_cap, al(wsd[name[id(L)]]), wn(wsd[name[id(L)]]), sp)
             else:
                 L.rle_decode_batch_device_sized(P(B.d_c), P(B.coffs), P(clen), P(B.d_out), P(B.offs), P(B.lens), None,
                                                 P(B.status), B.n, B.max_c, B.max_u, sp)
 
         res = {k: {"enc": [], "dec": [], "ok": True} for k in libs}
-        for k, L in libs.items():   # correctness of every build on this batch
-            B.d_out.zero_()
+        for k, L in libs.items():   # correctness of every build on this batch (outputs poisoned first)
+            B.d_out.copy_(B.d_in)
+            B.d_out[inmask] ^= 0xFF   # every decoded byte differs from the input until written
+            B.d_c.fill_(0xA5)
             enc(L)
             dec(L)
             torch.cuda.synchronize()
-            res[k]["ok"] = bool(torch.equal(B.d_out, B.d_in)) and bool(torch.equal(B.d_c, ref_c))
+            res[k]["ok"] = bool(torch.equal(B.d_out, B.d_in)) and bool(torch.equal(clen, ref_clen))
         for _ in range(a.rounds):
             for k, L in libs.items():
                 for kind, fn in (("enc", enc), ("dec", dec)):
