@@ -24,15 +24,14 @@ namespace rle {
 
 // Segment length: seg_tiles tiles of 1008 input bytes, a kernel argument chosen by the launcher
 // (4..64 tiles: about 16 segments per CU over the batch).
-#ifndef RLE_SEG_TILES_MAX
-#define RLE_SEG_TILES_MAX 64
+#ifndef RLE_SEG_TILES_MAX   // 16 since r3s (was 64): more, shorter segments fill the chip better
+#define RLE_SEG_TILES_MAX 16
 #endif
 constexpr u32 kSegTilesMin = 4, kSegTilesMax = RLE_SEG_TILES_MAX;
-// decode write pass staging (chunks per wave, rle_device.h kDecChunks): fewer -> more waves per SIMD
-#ifndef RLE_SEG_DEC_CHUNKS
-#define RLE_SEG_DEC_CHUNKS RLE_DEC_CHUNKS
-#endif
-constexpr u32 kSegDecChunks = RLE_SEG_DEC_CHUNKS;
+// decode write pass staging (chunks per wave, rle_device.h kDecChunks): the launcher takes the
+// one-pass 192-chunk kernel when every segment is resident at once, else the 96-chunk one (7 instead
+// of 4 workgroups per CU; r3s A/B: 1 MiB random -9 %, mixed batch -27 %, one 64 MiB file +7 % with 96)
+constexpr u32 kSegDecChunksOne = RLE_DEC_CHUNKS, kSegDecChunksMany = 96;
 constexpr u32 kSegWaves = 4;
 constexpr u32 kSegBlock = kWave * kSegWaves;
 constexpr u32 kNone = 0xFFFFFFFFu;
@@ -147,7 +146,8 @@ __device__ __forceinline__ bool walk_seg(u32x4 rs, u32 start, u32 ntiles, u32 la
     return walk_tiles(rs, start, ntiles, lane, mem, step);
 }
 
-// Resident segments (the single-pass kernels below): a segment of at most kResTiles tiles is loaded
+// Resident segments (the single-pass kernels below): a segment of at most kResTiles tiles (segments
+// are kResTiles - 1 tiles, a buffer's last one up to 2 bytes more) is loaded
 // into the wave's LDS region once, [p0, p0 + 1008 nt + 16) in 1 KiB LDS-DMAs (range-checked: zeros
 // past the buffer), and both its summary and its output walk read it there.
 #ifndef RLE_RES_TILES
@@ -155,6 +155,10 @@ __device__ __forceinline__ bool walk_seg(u32x4 rs, u32 start, u32 ntiles, u32 la
 #endif
 constexpr u32 kResTiles = RLE_RES_TILES;
 constexpr u32 kResBytes = (kResTiles * kTileStep + 16u + 1023u) & ~1023u;
+#ifndef RLE_RES_PAD   // debug: spare LDS bytes after each wave's region
+#define RLE_RES_PAD 0
+#endif
+constexpr u32 kResStride = kResBytes + RLE_RES_PAD;
 #ifndef RLE_RES_DEC_CHUNKS   // the resident decode's staging (chunks per wave; its region takes LDS too)
 #define RLE_RES_DEC_CHUNKS 96
 #endif
@@ -433,16 +437,20 @@ __device__ __forceinline__ u32 seg_lookback(u32 g, u32 s0, const u32* sflag, u32
         const u32 j = valid ? hi - 1u - lane : hi - 1u;
         u32 f = valid ? ld_relaxed(sflag + j) : kFlagAgg;
         u32 polls = 0;
-        while (__builtin_amdgcn_ballot_w64(f == 0u)) {
-            if (++polls > kSpinMax) {
-                late = true;
+        // wait only for the segments between this one and the nearest published inclusive state
+        // (or, when the window has none, for the whole window)
+        for (;;) {
+            const uint64_t m0 = __builtin_amdgcn_ballot_w64(f == 0u);
+            const uint64_t m2 = __builtin_amdgcn_ballot_w64(valid && f == kFlagIncl);
+            const uint64_t need = m2 ? (m2 & (0ull - m2)) - 1ull : ~0ull;
+            if (!(m0 & need) || ++polls > kSpinMax) {
+                if (m0 & need) late = true;
+                if (m2) return hi - (u32)__builtin_ctzll(m2);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
             if (f == 0u) f = ld_relaxed(sflag + j);
         }
-        const uint64_t m2 = __builtin_amdgcn_ballot_w64(valid && f == kFlagIncl);
-        if (m2) return hi - (u32)__builtin_ctzll(m2);
         if (lo == s0) return s0;
         hi = lo;
     }
@@ -529,17 +537,17 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
 
 
 // ---------------------------------------------------------------- resident single-pass encode
-// SURVEY.md §5's single pass, with the segment held in LDS: a wave takes kResTicket consecutive
-// segments per ticket (one global atomic per ticket, not per segment: a single counter serialises
-// its atomics, ~12-16 ns each, r3s), and for each segment loads its <= kResTiles tiles into its LDS
+// SURVEY.md §5's single pass, with the segment held in LDS: a wave takes a segment by ticket and loads its <= kResTiles tiles into its LDS
 // region once, summarises them there, publishes the summary, derives its entering state with the
 // decoupled look-back of the fused kernel above, publishes its inclusive state and walks the same
 // LDS tiles again to write.  HBM sees the input once.  Progress: as in the fused kernel, a wave
 // waits only on segments of earlier tickets, whose waves are running.
-#ifndef RLE_RES_TICKET
-#define RLE_RES_TICKET 4
-#endif
-constexpr u32 kResTicket = RLE_RES_TICKET;
+// One segment per ticket: a wave holding several consecutive segments publishes the later ones'
+// summaries only after writing the earlier ones, so the waves behind it in the same buffer wait for
+// its whole batch (measured: the look-backs run out of polls).  The next ticket is taken while the
+// current segment is processed, which hides the atomic's latency and keeps progress (a wave's
+// prefetched segment is always later than its current one).
+constexpr u32 kResTicket = 1;
 __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len,
@@ -551,24 +559,24 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
                                                                 const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                 uint4* __restrict__ summ, uint4* __restrict__ incl,
                                                                 u32* __restrict__ sflag, u32* __restrict__ ticket) {
-    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResStride];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kEncStage];
     __shared__ __attribute__((aligned(16))) u32 elut[kInsWaveWords];   // enc_tile_fast's selectors
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     uint8_t* stage = stage_all + wid * kEncStage;
-    const uint8_t* region = region_all + wid * kResBytes;
+    const uint8_t* region = region_all + wid * kResStride;
     for (u32 k = threadIdx.x; k < kInsWaveWords; k += kSegBlock) elut[k] = kEncInsLut.s[k];
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
+    u32 gnext = 0;
+    if (lane == 0) gnext = atomicAdd(ticket, 1u);
     for (;;) {
-        u32 g0 = 0;
-        if (lane == 0) g0 = atomicAdd(ticket, kResTicket);
-        g0 = uniform(g0);
-        if (g0 >= total) break;
-        const u32 g1 = g0 + kResTicket < total ? g0 + kResTicket : total;
-        for (u32 g = g0; g < g1; ++g) {
+        const u32 g = uniform(gnext);
+        if (g >= total) break;
+        if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
+        {
             const u32 b = uniform(seg_buf[g]);
             const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
             const uint64_t U64 = in_len[b];
@@ -817,6 +825,7 @@ __device__ __forceinline__ void dec_seg_write(const uint8_t* src, uint8_t* dst, 
     if (last && lane == 0 && st_b) *st_b = serial ? (RLE_STATUS_SERIAL | RLE_STATUS_OVERFLOW) : dec_tiled_status(st, U);
 }
 
+template <u32 kSegDecChunks>
 __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t* __restrict__ in,
                                                                   const uint64_t* __restrict__ in_off,
                                                                   const uint64_t* __restrict__ in_len,
@@ -894,7 +903,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
                                                                 u32* __restrict__ sflag, u32* __restrict__ ticket,
                                                                 u32* __restrict__ bflag) {
     constexpr u32 kStage = 32u * kResDecChunks;
-    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResStride];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kStage];
     __shared__ DecEntry tbl[256];
     __shared__ u32x4 clut[kCompactEntries];   // dec_tile_fast's selectors
@@ -905,18 +914,18 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
         clut[k] = u32x4{kCompactLut.s[4u * k], kCompactLut.s[4u * k + 1u], kCompactLut.s[4u * k + 2u],
                         kCompactLut.s[4u * k + 3u]};
     uint8_t* stage = stage_all + wid * kStage;
-    const uint8_t* region = region_all + wid * kResBytes;
+    const uint8_t* region = region_all + wid * kResStride;
     for (u32 k = lane; k < kStage / 16u; k += kWave) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
+    u32 gnext = 0;
+    if (lane == 0) gnext = atomicAdd(ticket, 1u);
     for (;;) {
-        u32 g0 = 0;
-        if (lane == 0) g0 = atomicAdd(ticket, kResTicket);
-        g0 = uniform(g0);
-        if (g0 >= total) break;
-        const u32 g1 = g0 + kResTicket < total ? g0 + kResTicket : total;
-        for (u32 g = g0; g < g1; ++g) {
+        const u32 g = uniform(gnext);
+        if (g >= total) break;
+        if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
+        {
             const u32 b = uniform(seg_buf[g]);
             const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
             const uint64_t C64 = in_len[b], U64 = out_len[b];
@@ -1062,8 +1071,10 @@ int device_cus(int* ncu) {
 #define RLE_SEG_TILES_FIX 0
 #endif
 // The resident single-pass kernels (enc_seg_res_kernel / dec_seg_res_kernel): RLE_MI355X_SEG_RES=1|0
-// overrides the build default.  Their segments are one LDS region's tiles, 16 bytes short, so that a
-// buffer's last segment (which absorbs a remainder of up to 2 bytes) still fits.
+// overrides the build default.  Their segments are one tile shorter than an LDS region, so that a
+// buffer's last segment (which absorbs a remainder of up to 2 bytes) still fits.  Segment lengths
+// stay whole tiles: a segment's exit state is read after the last tile's last lane (an 8048-byte
+// segment, measured, left the decode exit phase one lane late).
 #ifndef RLE_SEG_RES_DEFAULT
 #define RLE_SEG_RES_DEFAULT 0
 #endif
@@ -1075,7 +1086,7 @@ bool seg_res() {
     return on;
 }
 inline uint32_t seg_bytes(uint64_t total, int ncu) {
-    if (seg_res()) return rle::kResTiles * rle::kTileStep - 16u;
+    if (seg_res()) return (rle::kResTiles - 1u) * rle::kTileStep;
     if (RLE_SEG_TILES_FIX) return (uint32_t)RLE_SEG_TILES_FIX * rle::kTileStep;
     const uint64_t tiles = (total + rle::kTileStep - 1) / rle::kTileStep;
     uint64_t per = tiles / ((uint64_t)ncu * 16u);
@@ -1084,8 +1095,8 @@ inline uint32_t seg_bytes(uint64_t total, int ncu) {
 }
 // persistent grids: enough workgroups to fill every CU (RLE_SEG_OCC per CU), never more than the
 // segments
-#ifndef RLE_SEG_OCC
-#define RLE_SEG_OCC 4
+#ifndef RLE_SEG_OCC   // 24 since r3s (was 4): workgroups past residency queue behind the first ones
+#define RLE_SEG_OCC 24
 #endif
 inline uint32_t seg_grid(uint32_t maxseg, int ncu) {
     const uint32_t need = (maxseg + rle::kSegWaves - 1) / rle::kSegWaves;
@@ -1199,7 +1210,14 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
                        w.seg_first, w.seg_buf, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::dec_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
                        out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
-    hipLaunchKernelGGL(rle::dec_seg_write_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out,
-                       d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag);
+#ifndef RLE_SEG_DEC_FORCE   // A/B builds: 96 or 192 forces the decode write pass's staging
+#define RLE_SEG_DEC_FORCE 0
+#endif
+    const bool one_round = RLE_SEG_DEC_FORCE ? RLE_SEG_DEC_FORCE == 192
+                                             : maxseg <= (uint32_t)ncu * 16u;   // the 192-chunk kernel's residency
+    hipLaunchKernelGGL(one_round ? rle::dec_seg_write_kernel<rle::kSegDecChunksOne>
+                                 : rle::dec_seg_write_kernel<rle::kSegDecChunksMany>,
+                       dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out, d_out_off, d_out_len,
+                       d_out_cap, d_status, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }

@@ -104,6 +104,7 @@ def main():
                     e1.record(s)
                     torch.cuda.synchronize()
                     res[k][kind].append(e0.elapsed_time(e1) / a.reps * 1e3)
+                    print(f"  {wl} {k} {kind} {res[k][kind][-1]:.1f} us", file=sys.stderr, flush=True)
         for k in res:
             for kind in ("enc", "dec"):
                 v = sorted(res[k][kind])
