@@ -354,6 +354,68 @@ __device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, 
     wave_lds_sync();
 }
 
+// A segment without a run boundary (every byte equals the byte before the segment, v: zero-filled
+// data, long runs) encodes to "v v '9'" tokens every 9 bytes from the entering run start rs; only
+// the last token's count depends on the input, through the (up to 8) run bytes after the segment.
+// Its output is written from that alone, without reading the segment a second time (the summary
+// pass has read it): aligned 16-byte chunks of the 3-periodic pattern, and the partial chunks at
+// both ends, which the neighbouring segments share, bytewise.  (RLE_SEG_UNIFORM; round 3.)
+#ifndef RLE_SEG_UNIFORM
+#define RLE_SEG_UNIFORM 1
+#endif
+__device__ __forceinline__ void enc_seg_uniform(const uint8_t* src, uint8_t* dst, u32 U, u32 p0, u32 p1, u32 rs,
+                                                u32 off, u32 lane) {
+    const u32 v = src[p0];
+    const bool eq = lane < 8u && p1 + lane < U && src[p1 + lane] == v;
+    const u32 ext = (u32)__builtin_ctzll(__builtin_amdgcn_ballot_w64(!eq));   // run bytes past p1, <= 8
+    const u32 f = p0 + (9u - (p0 - rs) % 9u) % 9u;   // the segment's first token start
+    if (f >= p1) return;                             // none: the previous segment's token covers it
+    const u32 ns = (p1 - 1u - f) / 9u + 1u;
+    const u32 sl = f + 9u * (ns - 1u);
+    const u32 cl = p1 + ext - sl < 9u ? p1 + ext - sl : 9u;   // the last token's count
+    const u32 tot = 3u * (ns - 1u) + (cl >= 2u ? 3u : 1u);
+    const u32 end = off + tot;
+    const u32 ld = (cl >= 2u && cl < 9u) ? tot - 1u : ~0u;   // the output byte holding a count other than 9
+    const u32 vv = rep4(v), d9 = 0x39393939u;
+    auto byte_at = [&](u32 k) { return k % 3u != 2u ? v : (k == ld ? 0x30u + cl : 0x39u); };
+    // aligned interior chunks [a0, a1)
+    const u32 a0 = (off + 15u) & ~15u, a1 = end & ~15u;
+    const u32x4 rso = make_rsrc(dst, U + U / 2u);
+    for (u32 c0 = a0; c0 < a1; c0 += 16u * kWave) {
+        const u32 c = c0 + 16u * lane;
+        const u32 k0 = c - off, ph = k0 % 3u;
+        u32 o[4];
+#pragma unroll
+        for (u32 q = 0; q < 4u; ++q) {
+            u32 mk[3];
+#pragma unroll
+            for (u32 p = 0; p < 3u; ++p) {
+                u32 m = 0;
+                for (u32 b = 0; b < 4u; ++b)
+                    if ((p + 4u * q + b) % 3u == 2u) m |= 0xFFu << (8u * b);
+                mk[p] = m;
+            }
+            const u32 dm = ph == 0u ? mk[0] : ph == 1u ? mk[1] : mk[2];
+            o[q] = (vv & ~dm) | (d9 & dm);
+        }
+        const u32 kd = ld - k0;   // the odd count digit, when it falls in this chunk
+        if (kd < 16u) {
+            const u32 sh = 8u * (kd & 3u), q = kd >> 2;
+            const u32 dv = (0x30u + cl) << sh, msk = 0xFFu << sh;
+            o[0] = q == 0u ? (o[0] & ~msk) | dv : o[0];
+            o[1] = q == 1u ? (o[1] & ~msk) | dv : o[1];
+            o[2] = q == 2u ? (o[2] & ~msk) | dv : o[2];
+            o[3] = q == 3u ? (o[3] & ~msk) | dv : o[3];
+        }
+        vstore(rso, c < a1 ? c : kOOB, u32x4{o[0], o[1], o[2], o[3]}, false);
+    }
+    // the partial chunks at both ends
+    const u32 h1 = a0 < end ? a0 : end;
+    if (lane < 16u && off + lane < h1) dst[off + lane] = (uint8_t)byte_at(lane);
+    const u32 t0 = a1 > a0 ? a1 : a0;
+    if (lane < 16u && t0 + lane < end) dst[t0 + lane] = (uint8_t)byte_at(t0 + lane - off);
+}
+
 __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t* __restrict__ in,
                                                                   const uint64_t* __restrict__ in_off,
                                                                   const uint64_t* __restrict__ in_len,
@@ -361,7 +423,8 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
                                                                   const uint64_t* __restrict__ out_off, u32 n,
                                                                   const u32* __restrict__ seg_first, const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                   const uint2* __restrict__ plan,
-                                                                  const u32* __restrict__ bflag) {
+                                                                  const u32* __restrict__ bflag,
+                                                                  const uint4* __restrict__ summ) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kSegWaves * kEncStage];
     __shared__ __attribute__((aligned(16))) u32 elut[kInsWaveWords];   // enc_tile_fast's selectors
@@ -384,6 +447,13 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         u32 p0, p1;
         seg_range(g - s0, nseg, U, sb, p0, p1);
         const uint2 pl = plan[g];
+        if (RLE_SEG_UNIFORM && p0 > 0u) {
+            const uint4 sm = summ[g];
+            if (uniform(sm.y) == 0u && uniform(sm.x) == p1 - p0) {   // no run boundary in the segment
+                enc_seg_uniform(src, dst, U, p0, p1, uniform(pl.x), uniform(pl.y), lane);
+                continue;
+            }
+        }
         enc_seg_write(src, dst, U, p0, p1, uniform(pl.x), uniform(pl.y), lane, slots, stage, elut);
     }
 }
@@ -537,8 +607,8 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
 
 
 // ---------------------------------------------------------------- resident single-pass encode
-// SURVEY.md §5's single pass, with the segment held in LDS: a wave takes a segment by ticket and loads its <= kResTiles tiles into its LDS
-// region once, summarises them there, publishes the summary, derives its entering state with the
+// SURVEY.md §5's single pass, with the segment held in LDS: a wave takes a segment by ticket and
+// loads its <= kResTiles tiles into its LDS region once, summarises them there, publishes the summary, derives its entering state with the
 // decoupled look-back of the fused kernel above, publishes its inclusive state and walks the same
 // LDS tiles again to write.  HBM sees the input once.  Progress: as in the fused kernel, a wave
 // waits only on segments of earlier tickets, whose waves are running.
@@ -547,7 +617,6 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
 // its whole batch (measured: the look-backs run out of polls).  The next ticket is taken while the
 // current segment is processed, which hides the atomic's latency and keeps progress (a wave's
 // prefetched segment is always later than its current one).
-constexpr u32 kResTicket = 1;
 __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len,
@@ -1169,7 +1238,7 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     hipLaunchKernelGGL(rle::enc_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
                        out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
     hipLaunchKernelGGL(rle::enc_seg_write_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out,
-                       d_out_off, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag);
+                       d_out_off, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag, w.summ);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 

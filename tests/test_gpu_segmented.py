@@ -66,6 +66,22 @@ def test_large_buffers_per_kind(kind):
     _parity(xs)
 
 
+def test_uniform_segments():
+    """Segments without a run boundary are written from the entering run start alone (the write
+    pass does not read them again): runs from every phase, ending 0..10 bytes past a segment's end
+    (the last token's count), at the buffer's end, and whole zero-filled buffers, for every segment
+    length the launcher may pick at these sizes (multiples of 1008)."""
+    xs = []
+    for m in (4, 7, 16):
+        L = m * 1008
+        for e in range(11):
+            xs.append(O.gen(1, e, 100 + e) + b"z" * (3 * L + e) + O.gen(1, 50 + e, 3000))
+            xs.append(b"\x00" * (2 * L + e))
+        for ph in range(9):
+            xs.append(O.gen(1, 90 + ph, L - ph) + b"\xee" * (2 * L + 17) + b"\xef")
+    _parity(xs)
+
+
 def test_mixed_batch_same_as_one_wave_path():
     rng = np.random.default_rng(11)
     xs = []
