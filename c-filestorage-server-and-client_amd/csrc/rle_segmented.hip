@@ -2,8 +2,9 @@
 //
 // A one-wave-per-buffer launch walks a buffer's tiles one after another, so a single big buffer
 // (the drop-in's one-call-per-file path, src/filesystemApi.c:766-775, or the large end of a
-// mixed batch) runs at one wave's speed.  Here every buffer is cut into segments of 4..64 tiles
-// (1008 input bytes each; the launcher aims at ~16 segments per CU) that separate waves process.  The only state crossing a segment boundary is
+// mixed batch) runs at one wave's speed.  Here every buffer is cut into segments of 4..16 tiles
+// (1008 input bytes each; the launcher aims at ~16 segments per CU) that separate waves process.
+// The only state crossing a segment boundary is
 // (the algebra, checked against the oracle on CPU: tests/seg_model.py, tests/test_seg_model.py):
 //   encode  the run phase entering the segment.  A segment summary holds the offset L0 of its
 //           first run boundary, its last boundary lb, whether a boundary-free segment's run
@@ -14,16 +15,17 @@
 //           the three possible entry phases, the exit phase, the decoded byte count and whether
 //           the tiled path would decline; the per-buffer scan composes the exit maps (v_perm
 //           selectors, like the in-wave scan) and sums the counts of the phases actually taken.
-// Four launches per direction: plan (segments per buffer, exclusive scan), summary (persistent
-// waves over all segments), scan (one wave per buffer), write (persistent waves over all
+// Five launches per direction: plan (segments per buffer, exclusive scan), map (each segment's
+// buffer), summary (waves over all segments), scan (one wave per buffer), write (waves over all
 // segments, the tile steps of rle_device.h with absolute positions, an owned end and a first
-// chunk shared with the previous segment written bytewise).  Same output as rle_kernels.hip.
+// chunk shared with the previous segment written bytewise; encode writes a segment without a run
+// boundary from its entering state alone).  Same output as rle_kernels.hip.
 #include "rle_device.h"
 
 namespace rle {
 
 // Segment length: seg_tiles tiles of 1008 input bytes, a kernel argument chosen by the launcher
-// (4..64 tiles: about 16 segments per CU over the batch).
+// (4..16 tiles: about 16 segments per CU over the batch).
 #ifndef RLE_SEG_TILES_MAX   // 16 since r3s (was 64): more, shorter segments fill the chip better
 #define RLE_SEG_TILES_MAX 16
 #endif
@@ -1134,7 +1136,7 @@ int device_cus(int* ncu) {
     *ncu = c->second;
     return RLE_OK;
 }
-// segment length in bytes: about 16 segments per CU over the batch, 4..64 tiles each
+// segment length in bytes: about 16 segments per CU over the batch, 4..16 tiles each
 // (RLE_SEG_TILES_FIX > 0: a fixed segment length, for A/B builds)
 #ifndef RLE_SEG_TILES_FIX
 #define RLE_SEG_TILES_FIX 0
