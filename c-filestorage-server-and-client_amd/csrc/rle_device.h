@@ -1525,7 +1525,8 @@ constexpr DecCompactLut make_compact_lut() {
 static __constant__ DecCompactLut kCompactLut = make_compact_lut();
 
 // Returns the store instructions issued, or kNotFast (nothing done: the general path decodes the
-// tile).  Not for a segment's first chunk (st.head), nor with Co < C (one-wave walks only).
+// tile).  A segment's first tile only when nothing is staged yet; a segment's last tile (kTail,
+// Co < C on a tile edge) with its stores clipped at its output end (dec_tile_pr).
 // kTail (pr.tail): positions past C are neither starts nor kept, a pair whose digit lies past C
 // (the stream's final unbounded token) declines, and since the range check drops a store's dwords
 // that are not wholly below U (tools/probes/range_clip_probe.hip), the tile's last 4 output bytes
@@ -1535,7 +1536,8 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
                                              u32x4 rso, u32 U, DecState& st, const DecK& kc) {
     constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
     const u32* w = pr.w;
-    const u32 lim = kTail ? lowmask(pr.left < 16u ? pr.left : 16u) : 0xFFFFu;   // positions below C
+    // positions below the owned end (the stream's end C, or a segment's end on a tile edge)
+    const u32 lim = kTail ? lowmask(pr.lefto < 16u ? pr.lefto : 16u) : 0xFFFFu;
     const u32 NE16 = (pr.xa >> 7) | (pr.xb << 1);
     // cheap reject first (runs): at most 2 equal neighbours per owned lane
     if (__builtin_amdgcn_ballot_w64(__builtin_popcount(~NE16 & lim) > 2) & kOwned) return kNotFast;
@@ -1592,10 +1594,14 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     const u32 ttot = readlane(oincl, kWave - 1u);
     if (__builtin_amdgcn_ballot_w64(reject) & (RLE_DEC_DIGIT2 ? ~0ull : kOwned)) return kNotFast;
     if (kTail ? (ttot < 4u || st.out_pos + ttot > U) : st.out_pos + ttot + 16u > U) return kNotFast;
+    if (kTail) {
+        rso.z = uniform(st.out_pos + ttot);   // clip every store of this tile at its output end
+        asm volatile("s_nop 4" ::: "memory");   // (the descriptor word is fresh)
+    }
 
     u32 rounds = 0;
     const u32 rel0 = st.out_pos - st.flushed;
-    if (rel0) {   // a general tile's partial chunk: store it (its bytes past rel0 are rewritten below)
+    if (rel0 && !st.head) {   // a general tile's partial chunk: store it (its bytes past rel0 are rewritten below)
         u32x4 a, b;
         dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), a, b);
         u32 L[8];
@@ -1648,6 +1654,7 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     }
     st.out_pos += ttot;
     st.flushed = st.out_pos;
+    st.head = 0;   // (a segment's first tile: everything from its output offset on is stored)
     st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
     st.prev = readlane(w[3], kOwnLanes - 1u);
     return rounds + 1u;
@@ -1707,10 +1714,16 @@ template <bool kFast = false, u32 kChunks = kDecChunks>
 __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
                                            uint8_t* stage, uint8_t* dst, u32x4 rso, DecState& st, const DecK& kc,
                                            const u32x4* clut) {
-    // In a segment (Co < C) the literal path takes no tail tile: its tail form masks at the stream's
-    // end, not at the segment's, and its last store may reach past the tile's output, which only a
-    // later tile of the same wave rewrites (a segment's last tile is always a tail tile).
-    if (kFast && RLE_DEC_FAST && !st.head && (!pr.tail || Co == C)) {
+    // Segments (Co < C; rle_segmented.hip) end on tile edges, so their last tile (a tail tile) is a
+    // whole tile whose tail form clips its stores at its output end: the next segment's output is
+    // another wave's.  A segment's first tile takes the literal path when nothing is staged yet (its
+    // stores start at the segment's output offset, never before it).  RLE_DEC_SEGFAST=0: neither
+    // (round 2's rule: no literal path on a segment's first or last tile).
+#ifndef RLE_DEC_SEGFAST
+#define RLE_DEC_SEGFAST 1
+#endif
+    const bool head_ok = !st.head || (RLE_DEC_SEGFAST && st.out_pos - st.flushed == st.head);
+    if (kFast && RLE_DEC_FAST && head_ok && (!pr.tail || Co == C || RLE_DEC_SEGFAST)) {
         const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
                               : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
         if (r != kNotFast) return r;
