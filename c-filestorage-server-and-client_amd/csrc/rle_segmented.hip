@@ -43,8 +43,8 @@ constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the w
 #ifndef RLE_SEG_FAST   // the write passes take the fast tile paths (round 3); 0: general path only
 #define RLE_SEG_FAST 1
 #endif
-#ifndef RLE_SEG_REVERSE   // 1: the write passes take the segments last-summarised first (cache reuse: experiment)
-#define RLE_SEG_REVERSE 0
+#ifndef RLE_SEG_REVERSE   // the write passes take the segments last-summarised first (memory-side cache reuse)
+#define RLE_SEG_REVERSE 1   // r3w, same process: configs[2] mixed batch encode -6 %, decode -2 %; 1 MiB kinds +-1 %
 #endif
 #ifndef RLE_SEG_SUMFAST   // the summaries count uniform / literal tiles without the full analysis (round 3)
 #define RLE_SEG_SUMFAST 1
