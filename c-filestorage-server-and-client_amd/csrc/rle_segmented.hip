@@ -365,7 +365,15 @@ __device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, 
 #ifndef RLE_SEG_UNIFORM
 #define RLE_SEG_UNIFORM 1
 #endif
-__device__ __forceinline__ void enc_seg_uniform(const uint8_t* src, uint8_t* dst, u32 U, u32 p0, u32 p1, u32 rs,
+#ifndef RLE_SEG_UNIFORM_INLINE
+#define RLE_SEG_UNIFORM_INLINE 0
+#endif
+#if RLE_SEG_UNIFORM_INLINE
+#define RLE_SEG_UNIFORM_ATTR __forceinline__
+#else
+#define RLE_SEG_UNIFORM_ATTR __attribute__((noinline))   // out of the write loop's hot code (r3x)
+#endif
+__device__ RLE_SEG_UNIFORM_ATTR void enc_seg_uniform(const uint8_t* src, uint8_t* dst, u32 U, u32 p0, u32 p1, u32 rs,
                                                 u32 off, u32 lane) {
     const u32 v = src[p0];
     const bool eq = lane < 8u && p1 + lane < U && src[p1 + lane] == v;
@@ -382,7 +390,6 @@ __device__ __forceinline__ void enc_seg_uniform(const uint8_t* src, uint8_t* dst
     auto byte_at = [&](u32 k) { return k % 3u != 2u ? v : (k == ld ? 0x30u + cl : 0x39u); };
     // aligned interior chunks [a0, a1)
     const u32 a0 = (off + 15u) & ~15u, a1 = end & ~15u;
-    const u32x4 rso = make_rsrc(dst, U + U / 2u);
     for (u32 c0 = a0; c0 < a1; c0 += 16u * kWave) {
         const u32 c = c0 + 16u * lane;
         const u32 k0 = c - off, ph = k0 % 3u;
@@ -409,7 +416,7 @@ __device__ __forceinline__ void enc_seg_uniform(const uint8_t* src, uint8_t* dst
             o[2] = q == 2u ? (o[2] & ~msk) | dv : o[2];
             o[3] = q == 3u ? (o[3] & ~msk) | dv : o[3];
         }
-        vstore(rso, c < a1 ? c : kOOB, u32x4{o[0], o[1], o[2], o[3]}, false);
+        if (c < a1) *reinterpret_cast<u32x4*>(dst + c) = u32x4{o[0], o[1], o[2], o[3]};
     }
     // the partial chunks at both ends
     const u32 h1 = a0 < end ? a0 : end;
@@ -440,6 +447,9 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
         const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
+        // (the segment's own plan and summary load with its buffer index, not after it)
+        const uint2 pl = plan[g];
+        const uint4 sm = RLE_SEG_UNIFORM ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
         const u32 b = uniform(seg_buf[g]);
         if (uniform(bflag[b])) continue;
         const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
@@ -448,9 +458,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         uint8_t* dst = out + out_off[b];
         u32 p0, p1;
         seg_range(g - s0, nseg, U, sb, p0, p1);
-        const uint2 pl = plan[g];
         if (RLE_SEG_UNIFORM && p0 > 0u) {
-            const uint4 sm = summ[g];
             if (uniform(sm.y) == 0u && uniform(sm.x) == p1 - p0) {   // no run boundary in the segment
                 enc_seg_uniform(src, dst, U, p0, p1, uniform(pl.x), uniform(pl.y), lane);
                 continue;
@@ -738,11 +746,29 @@ __device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 l
 
 // One segment's decode summary: for each entry phase 0..2, the decoded bytes (.x .y .z) and, in .w,
 // the exit phases (2 bits each) and the phases whose tiled path declines (bits 8..10).  C > 0.
+// Whether every token starting in this tile (entry phase d, starts S80 from dec_lengths) carries
+// one byte v, the byte of the tile's first token.
+__device__ __forceinline__ bool dec_tile_single(const DecPrep& pr, const DecLen& ln, u32 d, const DecK& kc, u32& v) {
+    v = (readlane(pr.w[0], 0) >> (8u * d)) & 0xFFu;
+    const u32 vv = rep4(v);
+    u32 bad = 0;
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 t = pr.w[k] ^ vv;
+        bad |= bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80) & ln.S80[k];
+    }
+    return !owned_any(bad != 0u);
+}
+// One segment's decode summary: for each entry phase 0..2, the decoded bytes (.x .y .z) and, in .w,
+// the exit phases (2 bits each), the phases whose tiled path declines (bits 8..10) and the phases
+// from which every token carries one byte (bits 11..13: the segment decodes to copies of that byte,
+// the one at its first token; dec_seg_fill writes them without reading the segment).  C > 0.
 template <bool kRes = false>
 __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u32 q0, u32 q1, u32 lane,
                                                    const uint8_t* slots, const DecEntry* tbl) {
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
+    u32 uni = RLE_SEG_UNIFORM ? 7u : 0u, v0 = 0u, v1 = 0u, v2 = 0u;   // single-byte phases and their bytes
     const DecK kc = dec_k();
     walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
@@ -756,6 +782,15 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
                 const DecLen ln = dec_lengths(pr, d0);
                 tot = owned_sum(ln.nout);
                 bad = owned_any(ln.serial_lane);
+                if (uni) {
+                    u32 v;
+                    const bool one = dec_tile_single(pr, ln, d0, kc, v);
+                    if (!one || v != v0) uni &= ~1u;
+                    if (!one || v != v1) uni &= ~2u;
+                    if (!one || v != v2) uni &= ~4u;
+                }
+            } else {
+                uni = 0u;   // a literal tile (its own bytes, "v v 2" pairs): not counted as single-byte
             }
             c0 += tot; c1 += tot; c2 += tot;
             badm |= bad ? 7u : 0u;
@@ -770,13 +805,25 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
             const DecLen l2 = dec_lengths(pr, d2);
             c2 += owned_sum(l2.nout);
             badm |= owned_any(l2.serial_lane) ? 4u : 0u;
+            if (uni) {
+                u32 v;
+                bool one = dec_tile_single(pr, l0, d0, kc, v);
+                if (!one || (t && v != v0)) uni &= ~1u;
+                v0 = t ? v0 : v;
+                one = dec_tile_single(pr, l1, d1, kc, v);
+                if (!one || (t && v != v1)) uni &= ~2u;
+                v1 = t ? v1 : v;
+                one = dec_tile_single(pr, l2, d2, kc, v);
+                if (!one || (t && v != v2)) uni &= ~4u;
+                v2 = t ? v2 : v;
+            }
             d0 = bfe(m63, 8u * d0, 8);
             d1 = bfe(m63, 8u * d1, 8);
             d2 = bfe(m63, 8u * d2, 8);
         }
         return 0u;
     });
-    return make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8));
+    return make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8) | (uni << 11));
 }
 // the summary of an empty stream: counts 0, exit = entry
 constexpr uint4 kDecEmpty = {0u, 0u, 0u, 0u | (1u << 2) | (2u << 4)};
@@ -876,6 +923,23 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_scan_kernel(const uint8_t* 
     if (lane == 0) bflag[b] = c.serial ? kFlagSerial : 0u;
 }
 
+// A segment whose tokens all carry one byte v (summary bit 11 + e; never a stream's last segment,
+// whose end dec_finish handles) decodes to cnt copies of v: written without reading the segment,
+// aligned 16-byte chunks and, at both ends (shared with the neighbouring segments), single bytes.
+__device__ RLE_SEG_UNIFORM_ATTR void dec_seg_fill(uint8_t* dst, u32 U, u32 off, u32 cnt, u32 v, u32 lane) {
+    const u32 end = off + cnt;
+    const u32 a0 = (off + 15u) & ~15u, a1 = end & ~15u;
+    const u32 vv = rep4(v);
+    for (u32 c0 = a0; c0 < a1; c0 += 16u * kWave) {
+        const u32 c = c0 + 16u * lane;
+        if (c < a1) *reinterpret_cast<u32x4*>(dst + c) = u32x4{vv, vv, vv, vv};
+    }
+    const u32 h1 = a0 < end ? a0 : end;
+    if (lane < 16u && off + lane < h1) dst[off + lane] = (uint8_t)v;
+    const u32 t0 = a1 > a0 ? a1 : a0;
+    if (lane < 16u && t0 + lane < end) dst[t0 + lane] = (uint8_t)v;
+}
+
 // One segment's output: the tile walk from entry phase e and output offset off; the stream's last
 // segment (last) also writes the bytes up to U and the status (st_b, when given).
 template <bool kRes, u32 kChunks>
@@ -907,7 +971,8 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
                                                                   uint32_t* __restrict__ status, u32 n,
                                                                   const u32* __restrict__ seg_first, const u32* __restrict__ seg_buf, u32 maxseg, u32 sb,
                                                                   const uint2* __restrict__ plan,
-                                                                  const u32* __restrict__ bflag) {
+                                                                  const u32* __restrict__ bflag,
+                                                                  const uint4* __restrict__ summ) {
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kSegWaves * 2 * kSlot];
     constexpr u32 kStage = 32u * kSegDecChunks;
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kStage];
@@ -928,6 +993,8 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
         const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
+        const uint2 pl = plan[g];
+        const uint4 sm = RLE_SEG_UNIFORM ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
         const u32 b = uniform(seg_buf[g]);
         const u32 flag = uniform(bflag[b]);
         if (flag & kFlagSkip) continue;
@@ -945,7 +1012,14 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         }
         u32 q0, q1;
         seg_range(g - s0, nseg, C, sb, q0, q1);
-        const uint2 pl = plan[g];
+        if (RLE_SEG_UNIFORM && g + 1u != s0 + nseg) {   // one byte throughout: no second read
+            const u32 e = uniform(pl.x);
+            if ((uniform(sm.w) >> (11u + e)) & 1u) {
+                const u32 cnt = uniform(e == 0u ? sm.x : (e == 1u ? sm.y : sm.z));
+                dec_seg_fill(dst, U, uniform(pl.y), cnt, src[q0 + e], lane);
+                continue;
+            }
+        }
         dec_seg_write<false, kSegDecChunks>(src, dst, C, U, q0, q1, uniform(pl.x), uniform(pl.y), g + 1u == s0 + nseg,
                                             lane, slots, stage, tbl, clut, status ? status + b : nullptr);
     }
@@ -1289,6 +1363,6 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     hipLaunchKernelGGL(one_round ? rle::dec_seg_write_kernel<rle::kSegDecChunksOne>
                                  : rle::dec_seg_write_kernel<rle::kSegDecChunksMany>,
                        dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out, d_out_off, d_out_len,
-                       d_out_cap, d_status, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag);
+                       d_out_cap, d_status, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag, w.summ);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
