@@ -627,6 +627,14 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
 // its whole batch (measured: the look-backs run out of polls).  The next ticket is taken while the
 // current segment is processed, which hides the atomic's latency and keeps progress (a wave's
 // prefetched segment is always later than its current one).
+// RLE_RES_TICKETLESS (default): no ticket counter; wave w of workgroup k takes segment 4 k + w
+// of a grid of one wave per segment.  A workgroup is dispatched only after every lower-numbered
+// workgroup of its XCD, so the lowest-numbered waiting segment's predecessors are all running or
+// done, and the look-back cannot wait forever (and its polls are bounded regardless: a wave that
+// runs out marks its buffer and exits).
+#ifndef RLE_RES_TICKETLESS
+#define RLE_RES_TICKETLESS 1
+#endif
 __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len,
@@ -650,11 +658,13 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
     u32 gnext = 0;
-    if (lane == 0) gnext = atomicAdd(ticket, 1u);
+    if (RLE_RES_TICKETLESS) gnext = blockIdx.x * kSegWaves + wid;   // one segment per wave
+    else if (lane == 0) gnext = atomicAdd(ticket, 1u);
     for (;;) {
         const u32 g = uniform(gnext);
         if (g >= total) break;
-        if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
+        if (RLE_RES_TICKETLESS) gnext = total;
+        else if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
         {
             const u32 b = uniform(seg_buf[g]);
             const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
@@ -1065,11 +1075,13 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
     u32 gnext = 0;
-    if (lane == 0) gnext = atomicAdd(ticket, 1u);
+    if (RLE_RES_TICKETLESS) gnext = blockIdx.x * kSegWaves + wid;   // one segment per wave
+    else if (lane == 0) gnext = atomicAdd(ticket, 1u);
     for (;;) {
         const u32 g = uniform(gnext);
         if (g >= total) break;
-        if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
+        if (RLE_RES_TICKETLESS) gnext = total;
+        else if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
         {
             const u32 b = uniform(seg_buf[g]);
             const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
@@ -1291,7 +1303,8 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
                            maxseg, w.ticket, nullptr);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
-        hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+        hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
+                           dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, w.seg_buf, maxseg,
                            sb, w.summ, w.incl, w.sflag, w.ticket);
         return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
@@ -1339,7 +1352,8 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
                            maxseg, w.ticket, w.bflag);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
-        hipLaunchKernelGGL(rle::dec_seg_res_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
+        hipLaunchKernelGGL(rle::dec_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
+                           dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first,
                            w.seg_buf, maxseg, sb, w.summ, w.incl, w.sflag, w.ticket, w.bflag);
         hipLaunchKernelGGL(rle::dec_seg_serial_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off,
