@@ -333,6 +333,17 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32 pkmax(u32 a, u32 b) {
     return __builtin_bit_cast(u32, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
 }
+// packed u16 max against b's high half in both halves: {max(a.lo, b.hi), max(a.hi, b.hi)} -- one
+// v_pk_max_u16 with op_sel (the half selection folds into the source modifiers)
+__device__ __forceinline__ u32 pkmax_bhi(u32 a, u32 b) {
+    const us2 bv = __builtin_bit_cast(us2, b);
+    return __builtin_bit_cast(u32, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_shufflevector(bv, bv, 1, 1)));
+}
+// in-dword prefix max of a u16 pair: {a.lo, max(a.hi, a.lo)} -- one v_pk_max_u16 with op_sel_hi
+__device__ __forceinline__ u32 pkmax_lo2hi(u32 a) {
+    const us2 av = __builtin_bit_cast(us2, a);
+    return __builtin_bit_cast(u32, __builtin_elementwise_max(av, __builtin_shufflevector(av, av, 0, 0)));
+}
 
 // ---------------------------------------------------------------- diagnostic stamps
 // RLE_STAMPS=1 builds (never the product library) sum s_memtime cycles per decode segment in
@@ -1235,7 +1246,17 @@ __device__ __forceinline__ void dec_read_chunk(const u32x4* s4, u32x4& a, u32x4&
 __device__ __forceinline__ void dec_fill_scan(u32x4 a, u32x4 b, u32 (&L)[8]) {
     L[0] = a.x | 0x01000000u; L[1] = a.y | 0x03000200u; L[2] = a.z | 0x05000400u; L[3] = a.w | 0x07000600u;
     L[4] = b.x | 0x09000800u; L[5] = b.y | 0x0B000A00u; L[6] = b.z | 0x0D000C00u; L[7] = b.w | 0x0F000E00u;
-    if (!(RLE_ABL & 4)) {
+#ifndef RLE_FILL_OPSEL   // 1: the scan in 15 op_sel max instructions (0: round 2's 23, with v_perm)
+#define RLE_FILL_OPSEL 1
+#endif
+    if (RLE_FILL_OPSEL && !(RLE_ABL & 4)) {
+        // prefix max inside each dword (position 2m+1 takes 2m), then along the chunk: dword m takes
+        // the high half (position 2m-1, the prefix so far) of dword m-1 in both halves
+#pragma unroll
+        for (u32 m = 0; m < 8; ++m) L[m] = pkmax_lo2hi(L[m]);
+#pragma unroll
+        for (u32 m = 1; m < 8; ++m) L[m] = pkmax_bhi(L[m], L[m - 1]);
+    } else if (!(RLE_ABL & 4)) {
         // running max of the even positions (low halves) and of the odd ones (high halves) ...
 #pragma unroll
         for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], L[m - 1]);
