@@ -1268,8 +1268,12 @@ __device__ __forceinline__ void dec_fill_scan(u32x4 a, u32x4 b, u32 (&L)[8]) {
 }
 // The chunk's 16 output bytes: each position's latest key at or before it, else the byte `carry`
 // entering the chunk (a run entering a chunk covers at most its first 8 positions, dwords 0..3).
+__device__ __forceinline__ u32x4 dec_fill_out_rep(const u32 (&L)[8], u32 crep);
 __device__ __forceinline__ u32x4 dec_fill_out(const u32 (&L)[8], u32 carry) {
-    const u32 crep = carry | 0x10001000u | (carry << 16);
+    return dec_fill_out_rep(L, carry | 0x10001000u | (carry << 16));
+}
+// The carry as 0x10vv in both u16 halves (below every key, above every empty slot).
+__device__ __forceinline__ u32x4 dec_fill_out_rep(const u32 (&L)[8], u32 crep) {
     u32x4 o;
     o.x = __builtin_amdgcn_perm(pkmax(L[1], crep), pkmax(L[0], crep), 0x06040200u);
     o.y = __builtin_amdgcn_perm(pkmax(L[3], crep), pkmax(L[2], crep), 0x06040200u);
@@ -1278,10 +1282,16 @@ __device__ __forceinline__ u32x4 dec_fill_out(const u32 (&L)[8], u32 carry) {
     return o;
 }
 
+#ifndef RLE_FILL_CREP   // 1: the carry moves as the chunk's whole last dword, spread by one v_perm
+#define RLE_FILL_CREP 1
+#endif
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
                                          u32& head, uint8_t* dst, Stamps& sp) {
     const u32 rounds = (nfl + kWave - 1u) / kWave;
+    // the carry's fill halves (0x10 above the byte) in a VGPR, so the v_perm's selector can be the
+    // one constant-bus operand (no per-round v_mov)
+    const u32 k10 = RLE_FILL_CREP && rounds ? vconst(0x10101010u) : 0u;
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
         const bool active = c < nfl;
@@ -1298,8 +1308,17 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
         RLE_STAMP(sp, 3);   // flush: staging reads
         u32 L[8];
         dec_fill_scan(a, b, L);
-        const u32 lastb = (L[7] >> 16) & 0xFFu;   // byte of the chunk's last key = its last output byte
-        const u32x4 o = dec_fill_out(L, from_prev_lane(lastb, fillc));
+        // byte of the chunk's last key = its last output byte: bits 16..23 of L[7]
+        u32 lastb;
+        u32x4 o;
+        if (RLE_FILL_CREP) {
+            lastb = L[7];
+            const u32 prev = from_prev_lane(L[7], fillc << 16);
+            o = dec_fill_out_rep(L, __builtin_amdgcn_perm(prev, k10, 0x00060006u));
+        } else {
+            lastb = (L[7] >> 16) & 0xFFu;
+            o = dec_fill_out(L, from_prev_lane(lastb, fillc));
+        }
         RLE_STAMP(sp, 4);   // flush: fill + carry
         const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
         vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o, wt);   // RLE_NOSTORE: diagnostic
@@ -1319,7 +1338,7 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
             }
         }
         const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
-        fillc = readlane(lastb, lastlane);
+        fillc = RLE_FILL_CREP ? (readlane(lastb, lastlane) >> 16) & 0xFFu : readlane(lastb, lastlane);
         wave_lds_sync();
         RLE_STAMP(sp, 6);   // flush: re-zero + sync
     }
