@@ -1494,6 +1494,9 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
 #ifndef RLE_SCAT_MASK   // 1: the scatter writes token starts only (interior writes exec-masked off)
 #define RLE_SCAT_MASK 0
 #endif
+#ifndef RLE_SCAT_D16HI   // 1: the odd positions' keys stored from the high halves (no shifts);
+#define RLE_SCAT_D16HI 0   // measured neutral (r3j: 64 KiB runs50 -0.6 %, runs90 +0.3 %), off
+#endif
 // The scatter of one lane's decoded positions into the staging (2 bytes per position): endk = the
 // staging byte address of the lane's first decoded position.  u16 per position: the byte, with
 // the start flag (0x80) as the high byte: 0x80vv at a token start, an unflagged 0x00vv (ignored by
@@ -1512,16 +1515,23 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
             if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
             else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
         };
+        // the high u16 of key: ds_write_b16_d16_hi stores it without a shift (the compiler hoists
+        // the shifts out of the pass loop, where the d16_hi pattern no longer matches)
+        auto put_hi = [&put](u32 t, u32 key) {
+            if (RLE_SCAT_D16HI && !(RLE_ABL & 8))
+                asm volatile("ds_write_b16_d16_hi %0, %1" ::"v"(sswz(t)), "v"(key) : "memory");
+            else put(t, key >> 16);
+        };
         if (RLE_SCAT_MASK) {   // token starts only: the interior writes' lanes leave the bank conflicts
             if ((int)(xk_lo << 16) < 0) put(sub_byte<0>(endk, R), xk_lo);
-            if ((int)xk_lo < 0) put(sub_byte<1>(endk, R), xk_lo >> 16);
+            if ((int)xk_lo < 0) put_hi(sub_byte<1>(endk, R), xk_lo);
             if ((int)(xk_hi << 16) < 0) put(sub_byte<2>(endk, R), xk_hi);
-            if ((int)xk_hi < 0) put(sub_byte<3>(endk, R), xk_hi >> 16);
+            if ((int)xk_hi < 0) put_hi(sub_byte<3>(endk, R), xk_hi);
         } else {
             put(sub_byte<0>(endk, R), xk_lo);
-            put(sub_byte<1>(endk, R), xk_lo >> 16);
+            put_hi(sub_byte<1>(endk, R), xk_lo);
             put(sub_byte<2>(endk, R), xk_hi);
-            put(sub_byte<3>(endk, R), xk_hi >> 16);
+            put_hi(sub_byte<3>(endk, R), xk_hi);
         }
     }
 }
