@@ -1292,6 +1292,11 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
     // the carry's fill halves (0x10 above the byte) in a VGPR, so the v_perm's selector can be the
     // one constant-bus operand (no per-round v_mov)
     const u32 k10 = RLE_FILL_CREP && rounds ? vconst(0x10101010u) : 0u;
+#ifndef RLE_FLUSH_ZREG   // 1: the re-zeroing stores take a zero tuple held in VGPRs over the loop
+#define RLE_FLUSH_ZREG 1
+#endif
+    const u32x4 Z = RLE_FLUSH_ZREG && rounds ? u32x4{vconst(0u), vconst(0u), vconst(0u), vconst(0u)}
+                                             : u32x4{0u, 0u, 0u, 0u};
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
         const bool active = c < nfl;
@@ -1333,8 +1338,8 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
                 *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(s4))) = u32x4{0u, 0u, 0u, 0u};
                 *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(s4) + 16u)) = u32x4{0u, 0u, 0u, 0u};
             } else {
-                s4[0] = u32x4{0u, 0u, 0u, 0u};
-                s4[1] = u32x4{0u, 0u, 0u, 0u};
+                s4[0] = Z;
+                s4[1] = Z;
             }
         }
         const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
