@@ -324,14 +324,19 @@ def load_pmc(workload):
 
 
 # ------------------------------------------------------------------------------------ the exchange
+# Why "inline" is the default exchange mode: it is the only mode measured faster.
+XMODE_REASON = ("inline: measured 29.4 us per configs[1] step against 35.0 (async) and 45.0 (graph) in the "
+                "one-rank RCCL rehearsal (DESIGN.md s7, r3b); async's overlap of the gather is unmeasured at "
+                "N > 1 (one GPU per box), so it stays opt-in (RLE_BENCH_XMODE=async)")
 class Exchange:
     """The N > 1 exchange step of one rank: after a step's encode, its compressed
     sizes are all-gathered and scanned into global stream offsets.  Modes (RLE_BENCH_XMODE):
-      async    (default) one library call per step (rle_dist_gather_offsets_async): the gather +
-               scan run on a side stream after the step's encode, beside its decode and the next
-               step's encode; the codec stream waits only for the previous step's exchange;
-      inline   one library call (rle_dist_gather_offsets: ncclAllGather + the scan kernels) on the
-               codec's stream, between encode and decode;
+      inline   (default) one library call (rle_dist_gather_offsets: ncclAllGather + the scan
+               kernels) on the codec's stream, between encode and decode -- the measured-faster mode
+               (XMODE_REASON);
+      async    one library call per step (rle_dist_gather_offsets_async): the gather + scan run on
+               a side stream after the step's encode, beside its decode and the next step's encode;
+               the codec stream waits only for the previous step's exchange;
       graph    the inline calls captured with the whole timed loop in one HIP graph, the gather of
                step i on a graph branch beside decode i and encode i + 1;
       torch    shard.global_offsets (all_gather_into_tensor + cumsum) on a side stream: the fallback
@@ -486,7 +491,7 @@ def run_rank(args):
         stream = torch.cuda.current_stream()
         B = Batch(wl, rank, world, dev)
 
-    xmode = os.environ.get("RLE_BENCH_XMODE", "async")
+    xmode = os.environ.get("RLE_BENCH_XMODE", "inline")
     if xmode not in ("async", "inline", "graph"):
         raise SystemExit(f"RLE_BENCH_XMODE={xmode}: async, inline or graph")
     xch = Exchange(B, world, rank, dev, dry, xmode) if multi else None
@@ -578,7 +583,7 @@ def run_rank(args):
                "cpu_baseline": cpu, "north_star_dec64k": north, "concurrent_streams": conc}
         if xch is not None:
             out["exchange"] = {"mode": xch.mode, "offsets_match_process_group": offsets_ok, "graph_captured": graph_ok,
-                               "error": str(xch.error) if xch.error else None}
+                               "error": str(xch.error) if xch.error else None, "default_mode_reason": XMODE_REASON}
         if dry:
             out["dry_run"] = True
         print(json.dumps(out), flush=True)

@@ -26,8 +26,6 @@
 #include <string.h>
 
 #include <atomic>
-#include <mutex>
-#include <unordered_map>
 
 namespace rle {
 
@@ -350,31 +348,33 @@ std::atomic<int> g_coop_mode{[] {
 
 // Residency of one cooperative instantiation: workgroups per CU from the occupancy API (its LDS,
 // e.g. ~40-48 KB for dec_coop_kernel<W, 16384>, limits it well below the wave count), times the CUs
-// of the current device; each (kernel, device) pair is queried once.
-struct ResidencyCache {
-    std::mutex m;
-    std::unordered_map<uint64_t, uint64_t> blocks;   // key: kernel address ^ device
-} g_res;
-uint64_t resident_blocks(const void* kern, uint32_t threads) {
+// of the current device.  Each (kernel, device) pair is queried once and kept in a per-instantiation
+// atomic slot (value + 1; 0 = not queried yet), so the sized entry points -- every drop-in call of
+// every server worker thread -- read it without a lock (round 4: the round-3 form took one
+// process-wide mutex per launch).  Two threads racing on the first query both ask the API and store
+// the same value.
+constexpr int kResDevices = 64;
+template <auto Kern>
+uint64_t resident_blocks(uint32_t threads) {
+    static std::atomic<uint64_t> slot[kResDevices];
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    const uint64_t key = (uint64_t)(uintptr_t)kern ^ ((uint64_t)dev << 56);
-    std::lock_guard<std::mutex> g(g_res.m);
-    auto it = g_res.blocks.find(key);
-    if (it != g_res.blocks.end()) return it->second;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kResDevices) return 0;
+    const uint64_t v = slot[dev].load(std::memory_order_relaxed);
+    if (v) return v - 1u;
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)threads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)Kern, (int)threads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
         (void)hipGetLastError();
         per_cu = cus = 0;
     }
     const uint64_t r = (uint64_t)(per_cu > 0 ? per_cu : 0) * (uint64_t)(cus > 0 ? cus : 0);
-    g_res.blocks.emplace(key, r);
+    slot[dev].store(r + 1u, std::memory_order_relaxed);
     return r;
 }
-bool coop_admits(const void* kern, uint32_t threads, uint32_t n) {
+template <auto Kern>
+bool coop_admits(uint32_t threads, uint32_t n) {
     const int mode = g_coop_mode.load(std::memory_order_relaxed);
-    return mode == 0 ? false : mode == 1 ? true : (uint64_t)n <= resident_blocks(kern, threads);
+    return mode == 0 ? false : mode == 1 ? true : (uint64_t)n <= resident_blocks<Kern>(threads);
 }
 }  // namespace
 
@@ -391,7 +391,7 @@ extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off
     const dim3 g(n);
 #define RLE_ENC_COOP(W)                                                                                         \
     do {                                                                                                        \
-        if (!coop_admits((const void*)rle::enc_coop_kernel<W>, 64 * W, n)) return 0;                             \
+        if (!coop_admits<rle::enc_coop_kernel<W>>(64 * W, n)) return 0;                             \
         hipLaunchKernelGGL(rle::enc_coop_kernel<W>, g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off,     \
                            d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt);                   \
     } while (0)
@@ -418,7 +418,7 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
     const dim3 g(n);
 #define RLE_DEC_COOP(W, UM)                                                                                      \
     do {                                                                                                         \
-        if (!coop_admits((const void*)rle::dec_coop_kernel<W, UM>, 64 * W, n)) return 0;                          \
+        if (!coop_admits<rle::dec_coop_kernel<W, UM>>(64 * W, n)) return 0;                          \
         hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, \
                            d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt);         \
     } while (0)

@@ -14,7 +14,6 @@
 // librccl.so.1) or from an explicit path: the codec library links no second RCCL.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -190,35 +189,27 @@ void launch_scan(uint32_t grid, hipStream_t s, const int64_t* g, uint32_t world,
 #undef RLE_SCAN
 }
 
-// The tile sums' workspace, one per device.  It is allocated (or grown) by the first call that needs
-// it, so a caller that captures the exchange in a HIP graph makes one uncaptured call first (bench.py
-// verifies one step before it captures).
-constexpr int kMaxDevices = 64;
-int64_t* g_ws[kMaxDevices] = {};
-size_t g_ws_words[kMaxDevices] = {};
-pthread_mutex_t g_ws_lock = PTHREAD_MUTEX_INITIALIZER;
-int64_t* scan_workspace(size_t words) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
-    pthread_mutex_lock(&g_ws_lock);
-    if (g_ws_words[dev] < words) {
-        size_t w = g_ws_words[dev] ? g_ws_words[dev] : 4096;
-        while (w < words) w *= 2;
-        if (g_ws[dev]) (void)hipFree(g_ws[dev]);
-        g_ws[dev] = nullptr;
-        g_ws_words[dev] = 0;
-        if (hipMalloc((void**)&g_ws[dev], w * sizeof(int64_t)) == hipSuccess) g_ws_words[dev] = w;
-        else (void)hipGetLastError();
-    }
-    int64_t* p = g_ws[dev];
-    pthread_mutex_unlock(&g_ws_lock);
-    return p;
+// Tile sums of the whole-chip scan: tiles(n) int64 in the CALLER's workspace (round 4: a process-wide
+// workspace per device was shared by every caller, so two scans with n > kSmallK queued on different
+// streams of one device could write each other's tile sums, and a grown workspace was freed under a
+// HIP graph that had captured the old pointer).  Each caller now passes its own: exchanges that may
+// run at once (the two slots of shard.NativeExchange) use different workspaces, and a captured graph
+// keeps pointing at memory its owner keeps alive.
+uint32_t scan_tiles(uint32_t n, uint32_t* items_out) {
+    const uint32_t subtiles = (uint32_t)(((uint64_t)n + kScanThreads - 1) / kScanThreads);
+    const uint32_t items = (subtiles + kMaxTiles - 1) / kMaxTiles;
+    if (items_out) *items_out = items;
+    return (subtiles + items - 1) / items;
 }
 
 }  // namespace
 
+extern "C" size_t rle_dist_workspace_bytes(uint32_t n) {
+    return n <= kSmallK ? 0u : (size_t)scan_tiles(n, nullptr) * sizeof(int64_t);
+}
+
 extern "C" int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world, uint32_t n, int64_t* d_offsets,
-                                       void* stream) {
+                                       void* d_ws, size_t ws_bytes, void* stream) {
     if (!d_gathered || !d_offsets || world == 0) return RLE_E_INVAL;
     if (n == 0) return RLE_OK;
     const hipStream_t s = (hipStream_t)stream;
@@ -227,11 +218,10 @@ extern "C" int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world
                                    d_offsets);
         return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
     }
-    const uint32_t subtiles = (uint32_t)(((uint64_t)n + kScanThreads - 1) / kScanThreads);
-    const uint32_t items = (subtiles + kMaxTiles - 1) / kMaxTiles;
-    const uint32_t tiles = (subtiles + items - 1) / items;
-    int64_t* ws = scan_workspace(tiles);
-    if (!ws) return RLE_E_HIP;
+    uint32_t items = 0;
+    const uint32_t tiles = scan_tiles(n, &items);
+    if (!d_ws || ws_bytes < (size_t)tiles * sizeof(int64_t) || ((uintptr_t)d_ws & 7u)) return RLE_E_INVAL;
+    int64_t* ws = static_cast<int64_t*>(d_ws);
     hipLaunchKernelGGL(tile_sums_kernel, dim3(tiles), dim3(kScanThreads), 0, s, d_gathered, world, n, items, ws);
     launch_scan<kScanThreads>(tiles, s, d_gathered, world, n, items, ws, d_offsets);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
@@ -265,11 +255,12 @@ extern "C" int rle_dist_init(const void* id, size_t len, int rank, int world, co
 }
 
 extern "C" int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets,
-                                       void* stream) {
+                                       void* d_ws, size_t ws_bytes, void* stream) {
     if (!g_comm) return RLE_E_INVAL;
     if (!d_sizes || !d_gathered || !d_offsets) return RLE_E_INVAL;
+    if (ws_bytes < rle_dist_workspace_bytes(n) || (rle_dist_workspace_bytes(n) && !d_ws)) return RLE_E_INVAL;
     if (g_rccl.all_gather(d_sizes, d_gathered, n, kNcclInt64, g_comm, (hipStream_t)stream) != 0) return RLE_E_HIP;
-    return rle_dist_offsets_device(d_gathered, (uint32_t)g_world, n, d_offsets, stream);
+    return rle_dist_offsets_device(d_gathered, (uint32_t)g_world, n, d_offsets, d_ws, ws_bytes, stream);
 }
 
 // The exchange off the codec's stream: recorded after the encode issued on codec_stream so far, run
@@ -277,15 +268,21 @@ extern "C" int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64
 // here, before it issues the step's decode -- for the exchange of the OTHER slot, issued one call
 // earlier: so the sizes vector of that slot may be rewritten by the next step's encode.  The host
 // cost is this one call (events created once); the codec stream never waits for the gather it just
-// started.
+// started.  The events belong to the process's one communicator and one stream pair: calls must
+// alternate the slots (a repeated slot is RLE_E_INVAL: its codec-stream wait would be on the stale
+// other slot while the new encode may overwrite sizes the gather still reads), and the function is
+// not thread-safe.
 namespace {
 hipEvent_t g_ev_enc[2] = {}, g_ev_done[2] = {};
 bool g_done_rec[2] = {};
+int g_last_slot = -1;
 }  // namespace
 extern "C" int rle_dist_gather_offsets_async(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered,
-                                             int64_t* d_offsets, void* codec_stream, void* comm_stream, int slot) {
+                                             int64_t* d_offsets, void* d_ws, size_t ws_bytes, void* codec_stream,
+                                             void* comm_stream, int slot) {
     if (!g_comm) return RLE_E_INVAL;
     if (!d_sizes || !d_gathered || !d_offsets || (slot != 0 && slot != 1)) return RLE_E_INVAL;
+    if (slot == g_last_slot) return RLE_E_INVAL;
     for (int k = 0; k < 2; ++k) {
         if (!g_ev_enc[k] && hipEventCreateWithFlags(&g_ev_enc[k], hipEventDisableTiming) != hipSuccess) return RLE_E_HIP;
         if (!g_ev_done[k] && hipEventCreateWithFlags(&g_ev_done[k], hipEventDisableTiming) != hipSuccess) return RLE_E_HIP;
@@ -293,9 +290,10 @@ extern "C" int rle_dist_gather_offsets_async(const int64_t* d_sizes, uint32_t n,
     const hipStream_t cs = (hipStream_t)codec_stream, xs = (hipStream_t)comm_stream;
     if (hipEventRecord(g_ev_enc[slot], cs) != hipSuccess || hipStreamWaitEvent(xs, g_ev_enc[slot], 0) != hipSuccess)
         return RLE_E_HIP;
-    if (const int rc = rle_dist_gather_offsets(d_sizes, n, d_gathered, d_offsets, comm_stream)) return rc;
+    if (const int rc = rle_dist_gather_offsets(d_sizes, n, d_gathered, d_offsets, d_ws, ws_bytes, comm_stream)) return rc;
     if (hipEventRecord(g_ev_done[slot], xs) != hipSuccess) return RLE_E_HIP;
     g_done_rec[slot] = true;
+    g_last_slot = slot;
     if (g_done_rec[1 - slot] && hipStreamWaitEvent(cs, g_ev_done[1 - slot], 0) != hipSuccess) return RLE_E_HIP;
     return RLE_OK;
 }
@@ -307,6 +305,7 @@ extern "C" int rle_dist_finalize(void) {
         g_ev_enc[k] = g_ev_done[k] = nullptr;
         g_done_rec[k] = false;
     }
+    g_last_slot = -1;
     int rc = RLE_OK;
     if (g_comm && g_rccl.comm_destroy(g_comm) != 0) rc = RLE_E_HIP;
     g_comm = nullptr;

@@ -98,12 +98,14 @@ def lib():
     for f, a in (("rle_dist_available", [ctypes.c_char_p]),
                  ("rle_dist_unique_id", [vp, sz, ctypes.c_char_p]),
                  ("rle_dist_init", [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
-                 ("rle_dist_gather_offsets", [vp, u32, vp, vp, vp]),
-                 ("rle_dist_gather_offsets_async", [vp, u32, vp, vp, vp, vp, ctypes.c_int]),
-                 ("rle_dist_offsets_device", [vp, u32, u32, vp, vp]),
+                 ("rle_dist_gather_offsets", [vp, u32, vp, vp, vp, sz, vp]),
+                 ("rle_dist_gather_offsets_async", [vp, u32, vp, vp, vp, sz, vp, vp, ctypes.c_int]),
+                 ("rle_dist_offsets_device", [vp, u32, u32, vp, vp, sz, vp]),
                  ("rle_dist_finalize", [])):
         getattr(L, f).restype = ctypes.c_int
         getattr(L, f).argtypes = a
+    L.rle_dist_workspace_bytes.restype = sz
+    L.rle_dist_workspace_bytes.argtypes = [u32]
     _lib = L
     return L
 
@@ -339,23 +341,43 @@ def dist_init(uid: bytes, rank: int, world: int):
     _check(lib().rle_dist_init(uid, len(uid), rank, world, _torch_rccl_path()), "rle_dist_init")
 
 
-def dist_gather_offsets(sizes, gathered, offsets, stream=None):
+def dist_workspace(n: int, device):
+    """The scan workspace of one exchange of n sizes per rank (rle_dist_workspace_bytes): an int64
+    device tensor (at least one element), to be kept alive as long as any call or graph uses it.
+    Exchanges that may run at once need one each."""
+    words = max(1, int(lib().rle_dist_workspace_bytes(int(n))) // 8)
+    import torch
+    return torch.empty(words, dtype=torch.int64, device=device)
+
+
+def _ws(ws):
+    return (_ptr(ws), ws.numel() * ws.element_size()) if ws is not None else (None, 0)
+
+
+def dist_gather_offsets(sizes, gathered, offsets, stream=None, ws=None):
     """One exchange step (rle_dist_gather_offsets) on `stream`: sizes (int64[n], device) all-gathered
-    and scanned into offsets (int64[world * n]) in the global stream order."""
-    _check(lib().rle_dist_gather_offsets(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets),
+    and scanned into offsets (int64[world * n]) in the global stream order; ws: dist_workspace(n)."""
+    if ws is None:
+        ws = dist_workspace(sizes.numel(), sizes.device)
+    _check(lib().rle_dist_gather_offsets(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets), *_ws(ws),
                                          _stream_ptr(stream)), "rle_dist_gather_offsets")
 
 
-def dist_gather_offsets_async(sizes, gathered, offsets, codec_stream, comm_stream, slot: int):
+def dist_gather_offsets_async(sizes, gathered, offsets, codec_stream, comm_stream, slot: int, ws=None):
     """The exchange on comm_stream after the work issued on codec_stream (rle_dist_gather_offsets_async);
-    codec_stream waits only for the previous call's exchange (the other slot)."""
-    _check(lib().rle_dist_gather_offsets_async(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets),
+    codec_stream waits only for the previous call's exchange (the other slot).  Slots must alternate;
+    ws: this slot's dist_workspace(n)."""
+    if ws is None:
+        ws = dist_workspace(sizes.numel(), sizes.device)
+    _check(lib().rle_dist_gather_offsets_async(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets), *_ws(ws),
                                                _stream_ptr(codec_stream), _stream_ptr(comm_stream), int(slot)),
            "rle_dist_gather_offsets_async")
 
 
-def dist_offsets(gathered, world: int, n: int, offsets, stream=None):
-    _check(lib().rle_dist_offsets_device(_ptr(gathered), world, n, _ptr(offsets), _stream_ptr(stream)),
+def dist_offsets(gathered, world: int, n: int, offsets, stream=None, ws=None):
+    if ws is None:
+        ws = dist_workspace(n, gathered.device)
+    _check(lib().rle_dist_offsets_device(_ptr(gathered), world, n, _ptr(offsets), *_ws(ws), _stream_ptr(stream)),
            "rle_dist_offsets_device")
 
 

@@ -92,11 +92,13 @@ class NativeExchange:
         # is issued
         self.gathered = [torch.empty(world * n, dtype=torch.int64, device=dev) for _ in range(2)]
         self.offsets = [torch.empty(world * n, dtype=torch.int64, device=dev) for _ in range(2)]
+        # one scan workspace per slot: the two slots' exchanges may run at once (async / graph modes)
+        self.ws = [R.dist_workspace(n, dev) for _ in range(2)]
 
     def step(self, local_sizes: torch.Tensor, stream, slot: int = 0) -> torch.Tensor:
         """Issue one exchange on `stream` after the work issued on it so far, into result buffer
         `slot` (0 or 1); returns the offsets tensor (complete in stream order)."""
-        self.R.dist_gather_offsets(local_sizes, self.gathered[slot], self.offsets[slot], stream)
+        self.R.dist_gather_offsets(local_sizes, self.gathered[slot], self.offsets[slot], stream, ws=self.ws[slot])
         return self.offsets[slot]
 
     def step_async(self, local_sizes: torch.Tensor, codec_stream, comm_stream, slot: int) -> torch.Tensor:
@@ -104,7 +106,7 @@ class NativeExchange:
         codec_stream waits only for the previous call's exchange (rle_dist_gather_offsets_async).
         Callers alternate slot 0 / 1 per step."""
         self.R.dist_gather_offsets_async(local_sizes, self.gathered[slot], self.offsets[slot], codec_stream,
-                                         comm_stream, slot)
+                                         comm_stream, slot, ws=self.ws[slot])
         return self.offsets[slot]
 
     def close(self):

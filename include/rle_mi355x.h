@@ -162,23 +162,29 @@ int rle_mi355x_timeline(unsigned long long* out, int reset);
  *     d_sizes[n] into d_gathered[world * n] (rank major), then the exclusive scan in global order
  *     into d_offsets[world * n].
  *   rle_dist_offsets_device: the scan alone, on `stream` (tests).  Two launches over the whole
- *     chip; the first call on a device allocates a small workspace, so make one before capturing
- *     the exchange in a HIP graph.
+ *     chip, with the tile sums in the caller's workspace d_ws of ws_bytes >=
+ *     rle_dist_workspace_bytes(n) bytes (0 for n <= 512: d_ws may be NULL; 8-byte aligned).  Scans
+ *     that may run at once need workspaces of their own; a captured graph keeps the pointer, so the
+ *     caller keeps the workspace alive while the graph exists.  RLE_E_INVAL when it is too small.
  *   rle_dist_available: RLE_OK when the RCCL symbols resolve in this process (a preflight that every
  *     rank runs before any rank enters the blocking rle_dist_init).
  *   rle_dist_finalize: destroys the communicator. */
 int rle_dist_available(const char* rccl_path);
 int rle_dist_unique_id(void* out, size_t len, const char* rccl_path);
 int rle_dist_init(const void* id, size_t len, int rank, int world, const char* rccl_path);
-int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets,
-                            void* stream);
-int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world, uint32_t n, int64_t* d_offsets, void* stream);
+size_t rle_dist_workspace_bytes(uint32_t n);
+int rle_dist_gather_offsets(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets, void* d_ws,
+                            size_t ws_bytes, void* stream);
+int rle_dist_offsets_device(const int64_t* d_gathered, uint32_t world, uint32_t n, int64_t* d_offsets, void* d_ws,
+                            size_t ws_bytes, void* stream);
 /* rle_dist_gather_offsets off the codec's stream: after the work issued on codec_stream so far, the
  * gather + scan run on comm_stream into the caller's result buffers of `slot` (0 or 1, alternating
  * per step); codec_stream is made to wait only for the previous call's exchange (the other slot),
- * so the caller may rewrite the other slot's sizes in its next step. */
+ * so the caller may rewrite the other slot's sizes in its next step.  Each slot needs its own workspace
+ * (d_ws, as rle_dist_gather_offsets).  Calls must alternate the slots (a repeated slot is
+ * RLE_E_INVAL); one communicator and one stream pair per process; not thread-safe. */
 int rle_dist_gather_offsets_async(const int64_t* d_sizes, uint32_t n, int64_t* d_gathered, int64_t* d_offsets,
-                                  void* codec_stream, void* comm_stream, int slot);
+                                  void* d_ws, size_t ws_bytes, void* codec_stream, void* comm_stream, int slot);
 int rle_dist_finalize(void);
 
 /* Tests: the cooperative mode of the sized entry points, in-process (0 never, 1 whenever the sizes

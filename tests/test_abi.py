@@ -142,3 +142,15 @@ def test_fault_injection_only_in_test_build():
     th = os.path.join(os.path.dirname(R.LIB_PATH), "build", "librle_mi355x_testhooks.so")
     with open(th, "rb") as f:
         assert b"RLE_MI355X_FAIL_ALLOC_ABOVE" in f.read()
+
+
+def test_dist_scan_workspace_is_the_callers():
+    """The exchange's scan takes its tile sums in the caller's workspace: the size query
+    is host-only, and a missing or too-small workspace is refused before any launch."""
+    L = R.lib()
+    assert L.rle_dist_workspace_bytes(1) == 0 and L.rle_dist_workspace_bytes(512) == 0
+    w = L.rle_dist_workspace_bytes(131072)
+    assert w >= 8 and w % 8 == 0
+    fake = ctypes.c_void_p(0x1000)   # never dereferenced: the call must fail on the workspace check
+    assert L.rle_dist_offsets_device(fake, 8, 131072, fake, None, 0, None) == -1
+    assert L.rle_dist_offsets_device(fake, 8, 131072, fake, fake, w - 8, None) == -1

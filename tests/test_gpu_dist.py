@@ -57,7 +57,8 @@ def test_exchange_captured_in_graph_one_rank():
         sizes = torch.randint(1, 6000, (n,), dtype=torch.int64, device=DEV)
         gathered = torch.empty_like(sizes)
         offsets = torch.full((n,), -1, dtype=torch.int64, device=DEV)
-        R.dist_gather_offsets(sizes, gathered, offsets)   # eager first: allocates the scan workspace
+        ws = R.dist_workspace(n, DEV)   # the caller's: alive as long as the graph
+        R.dist_gather_offsets(sizes, gathered, offsets, ws=ws)
         torch.cuda.synchronize()
         offsets.fill_(-1)
         g = torch.cuda.CUDAGraph()
@@ -65,7 +66,7 @@ def test_exchange_captured_in_graph_one_rank():
         main.wait_stream(torch.cuda.current_stream())
         with torch.cuda.graph(g, stream=main, capture_error_mode="relaxed"):
             side.wait_stream(main)
-            R.dist_gather_offsets(sizes, gathered, offsets, side)
+            R.dist_gather_offsets(sizes, gathered, offsets, side, ws=ws)
             main.wait_stream(side)
         torch.cuda.synchronize()
         for _ in range(3):
@@ -113,12 +114,13 @@ def test_exchange_async_alternating_slots():
         sizes = [torch.zeros(n, dtype=torch.int64, device=DEV) for _ in range(2)]
         gathered = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(2)]
         offsets = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(2)]
+        ws = [R.dist_workspace(n, DEV) for _ in range(2)]
         want = []
         for i in range(6):
             s = i % 2
             v = torch.randint(1, 6000, (n,), dtype=torch.int64, device=DEV)
             sizes[s].copy_(v)   # the "encode" of step i, on the codec stream
-            R.dist_gather_offsets_async(sizes[s], gathered[s], offsets[s], codec, comm, s)
+            R.dist_gather_offsets_async(sizes[s], gathered[s], offsets[s], codec, comm, s, ws=ws[s])
             want.append(torch.cumsum(v, 0) - v)
             if i >= 4:
                 torch.cuda.synchronize()
@@ -126,3 +128,43 @@ def test_exchange_async_alternating_slots():
     finally:
         torch.cuda.synchronize()
         R.dist_finalize()
+
+
+def test_exchange_async_repeated_slot_refused():
+    """A repeated slot would make the codec stream wait on the stale other slot: refused."""
+    uid = R.dist_unique_id()
+    R.dist_init(uid, 0, 1)
+    try:
+        n = 1024
+        codec, comm = torch.cuda.current_stream(), torch.cuda.Stream()
+        sizes = torch.ones(n, dtype=torch.int64, device=DEV)
+        g = torch.empty(n, dtype=torch.int64, device=DEV)
+        o = torch.empty(n, dtype=torch.int64, device=DEV)
+        R.dist_gather_offsets_async(sizes, g, o, codec, comm, 0)
+        with pytest.raises(R.RLEError):
+            R.dist_gather_offsets_async(sizes, g, o, codec, comm, 0)
+        R.dist_gather_offsets_async(sizes, g, o, codec, comm, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(o, torch.arange(n, dtype=torch.int64, device=DEV))
+    finally:
+        torch.cuda.synchronize()
+        R.dist_finalize()
+
+
+def test_offsets_two_streams_own_workspaces():
+    """Two whole-chip scans (n > 512) queued at once on two streams, each with its own workspace
+    (the process-wide workspace let them overwrite each other's tile sums)."""
+    world, n = 8, 131072
+    rng = np.random.default_rng(7)
+    gs = [rng.integers(0, 70000, size=world * n, dtype=np.int64) for _ in range(2)]
+    d_g = [torch.from_numpy(g).to(DEV) for g in gs]
+    d_o = [torch.full((world * n,), -1, dtype=torch.int64, device=DEV) for _ in range(2)]
+    ws = [R.dist_workspace(n, DEV) for _ in range(2)]
+    st = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for rep in range(5):
+        for k in range(2):
+            R.dist_offsets(d_g[k], world, n, d_o[k], st[k], ws=ws[k])
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert np.array_equal(d_o[k].cpu().numpy(), _ref_offsets(gs[k], world, n))

@@ -16,14 +16,15 @@ out = {}
 for world, n in ((8, 131072), (1, 1 << 20), (8, 4096)):
     g = torch.randint(0, 70000, (world * n,), dtype=torch.int64, device="cuda")
     o = torch.empty_like(g)
-    R.dist_offsets(g, world, n, o)
+    ws = R.dist_workspace(n, g.device)
+    R.dist_offsets(g, world, n, o, ws=ws)
     torch.cuda.synchronize()
     ref = g.view(world, n).t().reshape(-1)
     assert torch.equal(o, torch.cumsum(ref, 0) - ref)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(20):
-        R.dist_offsets(g, world, n, o)
+        R.dist_offsets(g, world, n, o, ws=ws)
     b.record()
     torch.cuda.synchronize()
     out[f"{world}x{n}"] = round(a.elapsed_time(b) / 20 * 1e3, 2)
