@@ -45,7 +45,10 @@ def _stage_files(tmp):
 
 
 class Server:
-    def __init__(self, exe, tmp, cfg, env=None):
+    """settle: seconds to wait after the socket appears (a server that has been up for a moment:
+    the drop-in's background start-up, csrc/rle_dropin.cpp preinit_main, has run)."""
+
+    def __init__(self, exe, tmp, cfg, env=None, settle=0.0):
         self.tmp = tmp
         self.sock = os.path.join(tmp, "s.sk")
         conf = dict(cfg, SOCKETFILENAME=self.sock, LOGFILENAME=os.path.join(tmp, "logs.json"))
@@ -59,6 +62,8 @@ class Server:
             if self.p.poll() is not None or time.time() - t0 > 60:
                 raise RuntimeError("server did not start: " + self.p.stdout.read().decode(errors="replace"))
             time.sleep(0.05)
+        if settle:
+            time.sleep(settle)
 
     def client(self, *args):
         r = subprocess.run([CLIENT, "-f", self.sock, "-t", "0", *args], cwd=self.tmp, capture_output=True,
@@ -86,9 +91,9 @@ def _returned(root):
     return out
 
 
-def battery1(exe, tmp, env=None):
+def battery1(exe, tmp, env=None, settle=0.0):
     files = _stage_files(tmp)
-    srv = Server(exe, tmp, {"MAXSTORAGECAP": 128000000, "MAXFILECOUNT": 10000, "WORKERPOOLSIZE": 1}, env)
+    srv = Server(exe, tmp, {"MAXSTORAGECAP": 128000000, "MAXFILECOUNT": 10000, "WORKERPOOLSIZE": 1}, env, settle)
     t0 = time.perf_counter()
     try:
         f1, f2 = os.path.join(files, "file1"), os.path.join(files, "file2")
@@ -100,10 +105,10 @@ def battery1(exe, tmp, env=None):
     return _max_storage(text), _returned(os.path.join(tmp, "dest1")), _returned(os.path.join(tmp, "dest2")), wall
 
 
-def battery2(exe, tmp, env=None):
+def battery2(exe, tmp, env=None, settle=0.0):
     files = _stage_files(tmp)
     srv = Server(exe, tmp, {"MAXSTORAGECAP": 1000000, "MAXFILECOUNT": 10, "WORKERPOOLSIZE": 4,
-                            "REPLACEMENTALGO": 1}, env)
+                            "REPLACEMENTALGO": 1}, env, settle)
     b = lambda n: os.path.join(files, "bigfiles", n)
     try:
         srv.client("-W", f"{b('big2')},{b('randbig')}")

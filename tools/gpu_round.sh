@@ -6,6 +6,7 @@ TAG=${1:-round}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
+hostname > $O/host.txt
 timeout -k 10 900 python -u -m pytest $R/tests -m gpu -v -rA --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/status
 case $rc in 124|134|137|139) exit $rc;; esac

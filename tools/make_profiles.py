@@ -93,7 +93,10 @@ def main():
                          f"{rd/1e6:.1f} | {wr/1e6:.1f} | {(rd+wr)/1e6:.1f} |")
     with open(os.path.join(PROF, f"{tag}_pmc.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
-    traffic["_source"] = f"profiles/{tag}_pmc.md (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; bytes per launch)"
+    hp = os.path.join(src, "host.txt")
+    host = open(hp).read().split()[0] if os.path.exists(hp) else "unrecorded"
+    traffic["_source"] = (f"profiles/{tag}_pmc.md (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; bytes per launch; "
+                          f"GPU round {tag}, box {host}; a different process from the bench line's)")
     with open(os.path.join(PROF, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(table)
