@@ -36,6 +36,13 @@
 #include "rle_fileops.h"
 #include "rle_mi355x.h"
 
+// Measured-slower host-path variants (call coalescing, pipelined staging) are compiled only into the
+// test library (build/librle_mi355x_testhooks.so) and `make variant` builds, never into the product
+// librle_mi355x.so (the measurements are in DESIGN.md §6).
+#ifndef RLE_VARIANTS
+#define RLE_VARIANTS 0
+#endif
+
 namespace {
 
 pthread_once_t g_once = PTHREAD_ONCE_INIT;
@@ -102,7 +109,9 @@ constexpr int kPipeEvents = 16;
 // 19 / 20 us per compress / decompress call against 21 / 23 with one H2D + one D2H;
 // profiles/r1e_small.md).  RLE_MI355X_SMALL=copy selects the copying form.
 bool g_zerocopy = true;
+#if RLE_VARIANTS
 bool g_coalesce = false;   // concurrent zero-copy calls join one launch (submit); RLE_MI355X_COALESCE=1: on
+#endif
 size_t g_presize = 1u << 20;   // staging allocated with each thread context (presize); RLE_MI355X_PRESIZE
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 
@@ -194,11 +203,13 @@ void init_once() {
     if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
+#if RLE_VARIANTS
     if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
+#endif
     if (const char* e = getenv("RLE_MI355X_PRESIZE")) g_presize = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_STAGING")) {
         if (!strcmp(e, "pinned")) g_staging = Staging::Pinned;
-        else if (!strcmp(e, "pipe")) g_staging = Staging::Pipe;
+        else if (RLE_VARIANTS && !strcmp(e, "pipe")) g_staging = Staging::Pipe;
     }
 #if RLE_TEST_HOOKS
     if (const char* e = getenv("RLE_MI355X_FAIL_ALLOC_ABOVE")) g_fail_above = (size_t)strtoull(e, nullptr, 10);
@@ -544,6 +555,7 @@ void presize(Ctx* c) {
     }
 }
 
+#if RLE_VARIANTS
 // ---------------------------------------------------------------- coalescing of concurrent small calls
 // The server's worker threads (src/server.c:520-524) call the codec concurrently -- reads of
 // different files decode outside the store lock (src/filesystemApi.c:570 -> 597) -- and a 4 KiB
@@ -679,16 +691,21 @@ void submit(Ctx* c, Req* r) {
     if (r->result == ~0ull) throw std::bad_alloc();
 }
 
+#endif  // RLE_VARIANTS
+
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, U);
     size_t C;
+#if RLE_VARIANTS
     if (g_coalesce) {
         Req r;
         r.d_buf = c->d_zc; r.in_len = U; r.out_len = 0; r.cap = 0; r.dec = false; r.result = 0;
         submit(c, &r);
         C = r.result;
-    } else {
+    } else
+#endif
+    {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
@@ -711,12 +728,15 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, C);
     uint32_t st;
+#if RLE_VARIANTS
     if (g_coalesce) {
         Req r;
         r.d_buf = c->d_zc; r.in_len = C; r.out_len = U; r.cap = total; r.dec = true; r.result = 0;
         submit(c, &r);
         st = (uint32_t)r.result;
-    } else {
+    } else
+#endif
+    {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);

@@ -160,11 +160,11 @@ constexpr u32 kResBytes = (kResTiles * kTileStep + 16u + 1023u) & ~1023u;
 #ifndef RLE_RES_PAD   // debug: spare LDS bytes after each wave's region
 #define RLE_RES_PAD 0
 #endif
-constexpr u32 kResStride = kResBytes + RLE_RES_PAD;
+[[maybe_unused]] constexpr u32 kResStride = kResBytes + RLE_RES_PAD;
 #ifndef RLE_RES_DEC_CHUNKS   // the resident decode's staging (chunks per wave; its region takes LDS too)
 #define RLE_RES_DEC_CHUNKS 96
 #endif
-constexpr u32 kResDecChunks = RLE_RES_DEC_CHUNKS;
+[[maybe_unused]] constexpr u32 kResDecChunks = RLE_RES_DEC_CHUNKS;
 __device__ __forceinline__ void res_load(u32x4 rs, u32 p0, u32 nt, u32 lane, const uint8_t* region) {
     const u32 l0 = uniform(lds_addr(region));
     const u32 nd = uniform((nt * kTileStep + 16u + 1023u) >> 10);
@@ -468,6 +468,15 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
     }
 }
 
+// ================================================================ measured-slower variants
+// (RLE_VARIANTS builds only: the test library build/librle_mi355x_testhooks.so and `make variant`;
+// never the product librle_mi355x.so.  VERDICT r3 item 8.)  The fused single-pass encode and the
+// resident single-pass kernels are bit-exact and tested, but slower than the five-launch default
+// ("Round 3: segmented path"), so the product does not carry them.
+#ifndef RLE_VARIANTS
+#define RLE_VARIANTS 0
+#endif
+#if RLE_VARIANTS
 // ---------------------------------------------------------------- fused single-pass encode
 // One launch after the plan (SURVEY.md §5's single-pass form, with a decoupled look-back carry):
 // waves take segments in ticket order (a global counter), summarise their segment, publish the
@@ -716,6 +725,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
         }
     }
 }
+#endif  // RLE_VARIANTS
 
 // ================================================================ DECODE
 // Decoded bytes of a non-tail tile entered at phase d when every pair token in it is "v v 2" (random
@@ -769,6 +779,7 @@ __device__ __forceinline__ bool dec_tile_single(const DecPrep& pr, const DecLen&
     }
     return !owned_any(bad != 0u);
 }
+
 // One segment's decode summary: for each entry phase 0..2, the decoded bytes (.x .y .z) and, in .w,
 // the exit phases (2 bits each), the phases whose tiled path declines (bits 8..10) and the phases
 // from which every token carries one byte (bits 11..13: the segment decodes to copies of that byte,
@@ -1036,6 +1047,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
 }
 
 
+#if RLE_VARIANTS
 // ---------------------------------------------------------------- resident single-pass decode
 // The decode form of enc_seg_res_kernel: a segment's summary is its three entry phases' counts and
 // exits (dec_seg_summarize), its entering phase and offset come from the look-back (dec_seg_window
@@ -1156,6 +1168,8 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_serial_kernel(const uint8_t
     if (lane == 0 && status) status[b] = stat;
 }
 
+#endif  // RLE_VARIANTS
+
 }  // namespace rle
 
 // ================================================================ C-ABI launchers
@@ -1236,6 +1250,7 @@ int device_cus(int* ncu) {
 #define RLE_SEG_RES_DEFAULT 0
 #endif
 bool seg_res() {
+    if (!RLE_VARIANTS) return false;   // (product build: RLE_MI355X_SEG_RES is not read)
     static const bool on = [] {
         const char* e = getenv("RLE_MI355X_SEG_RES");
         return e ? e[0] != '0' : RLE_SEG_RES_DEFAULT != 0;
@@ -1267,7 +1282,8 @@ inline uint32_t buf_grid(uint32_t n) { return (n + rle::kSegWaves - 1) / rle::kS
 #ifndef RLE_SEG_FUSED_DEFAULT
 #define RLE_SEG_FUSED_DEFAULT 0
 #endif
-bool seg_fused() {
+[[maybe_unused]] bool seg_fused() {
+    if (!RLE_VARIANTS) return false;   // (product build: RLE_MI355X_SEG_FUSED is not read)
     static const bool on = [] {
         const char* e = getenv("RLE_MI355X_SEG_FUSED");
         return e ? e[0] != '0' : RLE_SEG_FUSED_DEFAULT != 0;
@@ -1298,6 +1314,7 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
+#if RLE_VARIANTS
     if (seg_res()) {
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
                            maxseg, w.ticket, nullptr);
@@ -1317,6 +1334,7 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
                            w.incl, w.sflag, w.ticket);
         return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
     }
+#endif
     const uint32_t grid = seg_grid(maxseg, ncu);
     hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
                        nullptr, nullptr);
@@ -1347,6 +1365,7 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     if (!d_workspace || workspace_bytes < w.bytes) return RLE_E_INVAL;
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
+#if RLE_VARIANTS
     if (seg_res()) {
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
                            maxseg, w.ticket, w.bflag);
@@ -1360,6 +1379,7 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
                            d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.bflag);
         return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
     }
+#endif
     const uint32_t grid = seg_grid(maxseg, ncu);
     hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
                        nullptr, nullptr);

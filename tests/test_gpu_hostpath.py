@@ -48,9 +48,16 @@ print("ok", R.dropin_stats())
 '''
 
 
+# call coalescing and pipelined staging are measured slower than the defaults and live only in the
+# test build (RLE_VARIANTS, c-filestorage-server-and-client_amd/Makefile), not in the product library
+VARIANTS_LIB = os.path.join(ROOT, "c-filestorage-server-and-client_amd", "build", "librle_mi355x_testhooks.so")
+
+
 @pytest.mark.parametrize("mode", ["direct", "pinned", "pipe"])
 def test_staging_modes_bit_exact(mode):
     env = dict(os.environ, RLE_MI355X_STAGING=mode, RLE_MI355X_STAGE_CAP=str(1 << 20))
+    if mode == "pipe":
+        env["RLE_MI355X_LIB"] = VARIANTS_LIB
     r = subprocess.run([sys.executable, "-c", _STAGING_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
@@ -94,7 +101,7 @@ def test_concurrent_small_calls_coalesced_bit_exact():
     """With call coalescing on (RLE_MI355X_COALESCE=1, read at init: a fresh process): 16 Python
     threads, each 40 round trips of its own 4 KiB - 40 KiB buffers through the drop-in, every stream
     against the oracle; the library counts every small call as combined."""
-    env = dict(os.environ, RLE_MI355X_COALESCE="1")
+    env = dict(os.environ, RLE_MI355X_COALESCE="1", RLE_MI355X_LIB=VARIANTS_LIB)
     r = subprocess.run([sys.executable, "-c", _COALESCE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
@@ -127,8 +134,8 @@ def test_concurrent_small_calls_per_thread_streams_bit_exact():
 
 @pytest.mark.parametrize("coalesce", ["0", "1"])
 def test_callrate_tool_round_trips(coalesce):
-    """The C call-rate tool (8 threads x 4 KiB, 1 s): every round trip exact, with and without
-    call coalescing; with it, fewer launches than calls."""
+    """The C call-rate tool (8 threads x 4 KiB, 1 s) on the product library: every round trip exact;
+    RLE_MI355X_COALESCE=1 is not read by the product build (no call is combined)."""
     exe = os.path.join(ROOT, "tools", "callrate")
     assert os.path.exists(exe), "build() compiles tools/callrate"
     r = subprocess.run([exe, "8", "4096", "1"], capture_output=True, text=True, timeout=60,
@@ -136,7 +143,4 @@ def test_callrate_tool_round_trips(coalesce):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["bad"] == 0 and out["calls"] > 0
-    if coalesce == "1":
-        assert out["launches_coalesced"] < out["calls_coalesced"]
-    else:
-        assert out["calls_coalesced"] == 0
+    assert out["calls_coalesced"] == 0

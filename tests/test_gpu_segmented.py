@@ -143,6 +143,14 @@ print("ok")
 '''
 
 
+def _variants_lib(root):
+    """The fused and resident kernels are measured slower than the default and live only in the test
+    build (RLE_VARIANTS, c-filestorage-server-and-client_amd/Makefile), not in the product library."""
+    p = os.path.join(root, "c-filestorage-server-and-client_amd", "build", "librle_mi355x_testhooks.so")
+    assert os.path.exists(p), "build() makes the test library"
+    return p
+
+
 def test_fused_single_pass_encode():
     """The fused single-pass segmented encode (RLE_MI355X_SEG_FUSED=1, read at load: a fresh
     process): ticket-ordered segments, write-through summaries and inclusive states, the decoupled
@@ -153,7 +161,7 @@ def test_fused_single_pass_encode():
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
-    env = dict(os.environ, RLE_MI355X_SEG_FUSED="1")
+    env = dict(os.environ, RLE_MI355X_SEG_FUSED="1", RLE_MI355X_LIB=_variants_lib(root))
     r = subprocess.run([sys.executable, "-c", _FUSED_CODE, os.path.join(root, "c-filestorage-server-and-client_amd"),
                         os.path.join(root, "oracle"), here], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
@@ -168,7 +176,7 @@ def test_resident_single_pass():
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, RLE_MI355X_SEG_RES="1")
+    env = dict(os.environ, RLE_MI355X_SEG_RES="1", RLE_MI355X_LIB=_variants_lib(os.path.dirname(here)))
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
                         os.path.join(here, "test_gpu_segmented.py"), "-k", "not fused and not resident"],
                        env=env, capture_output=True, text=True, timeout=300)
