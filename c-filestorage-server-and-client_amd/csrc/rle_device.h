@@ -1205,6 +1205,7 @@ struct DecState {
     u32 prev;      // stream byte before the current tile, in bits 24..31
     bool wt;       // write-through output stores (vstore)
     Stamps sp;     // diagnostic builds only
+    u32 lit_skip = 0;   // tiles left before the literal path is tried again (RLE_DEC_LITSKIP)
 };
 
 // Bank spread of the decode staging (RLE_SWZ).  Unswizzled, a random-data tile decodes 16 positions
@@ -1470,6 +1471,9 @@ __device__ __forceinline__ DecLen dec_lengths_t(const DecPrep& p, u32 d) {
         }
     }
     u32 bad = 0u, sum = 0u;
+#ifndef RLE_SCAT_NEXT   // 1 (round 4): interior positions of dwords 0..2 write at the next token's slot (dec_scatter)
+#define RLE_SCAT_NEXT 1
+#endif
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 P80 = bitop3<0xF0 & ~0xCC & 0xAA>(S80[k], p.g[k], VD80[k]);   // 3-byte start, digit in stream
@@ -1482,7 +1486,8 @@ __device__ __forceinline__ DecLen dec_lengths_t(const DecPrep& p, u32 d) {
         const u32 S01 = fshr<7>(S80[k]);
         r.S80[k] = S80[k];
         r.S01[k] = S01;
-        r.N02[k] = fsub(O02[k], fshr<6>(S80[k]));
+        // (only dword 3 needs it with RLE_SCAT_NEXT: dec_scatter)
+        r.N02[k] = (RLE_SCAT_NEXT && k < 3u) ? 0u : fsub(O02[k], fshr<6>(S80[k]));
         r.W[k] = fadd(S01, b & P7F);
         sum = fadd(sum, r.W[k]);
     }
@@ -1505,7 +1510,14 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
 // The scatter of one lane's decoded positions into the staging (2 bytes per position): endk = the
 // staging byte address of the lane's first decoded position.  u16 per position: the byte, with
 // the start flag (0x80) as the high byte: 0x80vv at a token start, an unflagged 0x00vv (ignored by
-// the fill) anywhere else.
+// the fill) anywhere else.  Where an interior position (a 3-byte token's second byte or count digit)
+// writes its unflagged key: RLE_SCAT_NEXT (round 4), positions 0..13 at the slot right after their
+// own token's output, which is the next token's start slot: that token starts in the same lane (a
+// token spans at most 3 positions), whose later write of the flagged key (program order) replaces
+// it; positions 14 and 15, whose next token may start in the next lane (written by an earlier
+// instruction there), keep round 3's rule: one slot back, their own token's last decoded position,
+// which never holds a key (counts are >= 2 on this path).  Saves the N02 / R arithmetic of three of
+// the four dwords.
 __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 endk) {
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
@@ -1778,10 +1790,21 @@ __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u3
 #define RLE_DEC_SEGFAST 1
 #endif
     const bool head_ok = !st.head || (RLE_DEC_SEGFAST && st.out_pos - st.flushed == st.head);
+    // A tile that fails the literal path's test makes the next RLE_DEC_LITSKIP tiles skip it (round 4):
+    // run-heavy data (runs50 / runs90) fails it on every tile, paying its reject test (~7 VALU and
+    // ~10 SALU) for nothing; a buffer that turns literal again is found within that many tiles.
+#ifndef RLE_DEC_LITSKIP
+#define RLE_DEC_LITSKIP 3
+#endif
     if (kFast && RLE_DEC_FAST && head_ok && (!pr.tail || Co == C || RLE_DEC_SEGFAST)) {
-        const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
-                              : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
-        if (r != kNotFast) return r;
+        if (RLE_DEC_LITSKIP && st.lit_skip && !pr.tail) {
+            --st.lit_skip;
+        } else {
+            const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
+                                  : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
+            if (r != kNotFast) return r;
+            st.lit_skip = RLE_DEC_LITSKIP;
+        }
     }
     const DecLen ln = dec_lengths(pr, st.d);
     const u32* w = pr.w;
