@@ -1790,11 +1790,11 @@ __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u3
 #define RLE_DEC_SEGFAST 1
 #endif
     const bool head_ok = !st.head || (RLE_DEC_SEGFAST && st.out_pos - st.flushed == st.head);
-    // A tile that fails the literal path's test makes the next RLE_DEC_LITSKIP tiles skip it (round 4):
-    // run-heavy data (runs50 / runs90) fails it on every tile, paying its reject test (~7 VALU and
-    // ~10 SALU) for nothing; a buffer that turns literal again is found within that many tiles.
-#ifndef RLE_DEC_LITSKIP
-#define RLE_DEC_LITSKIP 3
+    // RLE_DEC_LITSKIP > 0: a tile that fails the literal path's test makes the next that many tiles
+    // skip it (round-4 experiment): run-heavy data (runs50 / runs90) fails it on every tile, paying
+    // its reject test (~7 VALU and ~10 SALU) for nothing.
+#ifndef RLE_DEC_LITSKIP   // 0 (off): measured r4a, same process: runs50 -1 %, but configs[1] decode +8 %
+#define RLE_DEC_LITSKIP 0     // and 64 KiB random +2 % (the extra loop state changes the code)
 #endif
     if (kFast && RLE_DEC_FAST && head_ok && (!pr.tail || Co == C || RLE_DEC_SEGFAST)) {
         if (RLE_DEC_LITSKIP && st.lit_skip && !pr.tail) {

@@ -27,7 +27,6 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <new>
 #include <mutex>
 #include <vector>
@@ -164,7 +163,9 @@ constexpr size_t kMetaDec = 0, kMetaEnc = 8, kMetaApp = 16, kMetaSlots = 24;
 // context touches HIP any more (the OS reclaims the memory); the lock orders the two.
 pthread_mutex_t g_exit_lock = PTHREAD_MUTEX_INITIALIZER;
 bool g_exiting = false;
+void preinit_join();   // below
 void on_exit_handler() {
+    preinit_join();   // (when called from the start-up thread's own exit: never; it makes no exit call)
     pthread_mutex_lock(&g_exit_lock);
     g_exiting = true;
     pthread_mutex_unlock(&g_exit_lock);
@@ -258,17 +259,23 @@ Ctx* new_ctx(int dev) {
 // makes its own only when the pool is empty.  Process exit stops the thread between two steps and
 // waits for it (preinit_exit, registered before the thread starts), so it never runs into the
 // runtime's teardown.
-std::mutex g_pool_m;
-std::condition_variable g_pool_cv;
-std::vector<Ctx*> g_pool;
+// Everything the start-up thread touches is constant-initialised (POD, pthread static
+// initialisers): the constructor that starts it may run before this file's dynamic initialisers
+// (a std::vector pool re-initialised under the running thread corrupted the heap, r4a e2e run).
+constexpr int kPoolMax = 64;
+pthread_mutex_t g_pool_m = PTHREAD_MUTEX_INITIALIZER;
+pthread_cond_t g_pool_cv = PTHREAD_COND_INITIALIZER;
+Ctx* g_pool[kPoolMax];
+int g_pool_n = 0;                    // under g_pool_m
 bool g_pre_running = false;          // under g_pool_m
 std::atomic<bool> g_pre_stop{false};
 pthread_t g_pre_thread;
-bool g_pre_started = false;
+std::atomic<bool> g_pre_started{false};
 
 void* preinit_main(void*) {
     int want = 8;
     if (const char* e = getenv("RLE_MI355X_PREINIT")) want = atoi(e);
+    want = want < kPoolMax ? want : kPoolMax;
     pthread_once(&g_once, init_once);
     for (int i = 0; i < want && g_ndev > 0 && !g_pre_stop.load(); ++i) {
         const int dev = (g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev);
@@ -280,38 +287,42 @@ void* preinit_main(void*) {
             if (c) free_ctx(c);
             break;
         }
-        std::lock_guard<std::mutex> g(g_pool_m);
-        g_pool.push_back(c);
-        g_pool_cv.notify_all();
+        pthread_mutex_lock(&g_pool_m);
+        g_pool[g_pool_n++] = c;
+        pthread_cond_broadcast(&g_pool_cv);
+        pthread_mutex_unlock(&g_pool_m);
     }
-    std::lock_guard<std::mutex> g(g_pool_m);
+    pthread_mutex_lock(&g_pool_m);
     g_pre_running = false;
-    g_pool_cv.notify_all();
+    pthread_cond_broadcast(&g_pool_cv);
+    pthread_mutex_unlock(&g_pool_m);
     return nullptr;
 }
-void preinit_exit() {
+// Stops the start-up thread between two steps and waits for it.  Called from on_exit_handler, which
+// init_once registers right after the runtime's first call, so it runs before any exit hook the
+// runtime registered while starting up; preinit_exit (registered by the constructor) is the
+// fallback for a process that exits before that.
+void preinit_join() {
     g_pre_stop.store(true);
-    if (g_pre_started) {
-        pthread_join(g_pre_thread, nullptr);
-        g_pre_started = false;
-    }
+    if (g_pre_started.exchange(false)) pthread_join(g_pre_thread, nullptr);
 }
+void preinit_exit() { preinit_join(); }
 __attribute__((constructor)) void preinit_start() {
     const char* e = getenv("RLE_MI355X_PREINIT");
     if (e && atoi(e) <= 0) return;
     atexit(preinit_exit);
-    std::lock_guard<std::mutex> g(g_pool_m);
+    pthread_mutex_lock(&g_pool_m);
     g_pre_running = true;
-    if (pthread_create(&g_pre_thread, nullptr, preinit_main, nullptr) == 0) g_pre_started = true;
+    if (pthread_create(&g_pre_thread, nullptr, preinit_main, nullptr) == 0) g_pre_started.store(true);
     else g_pre_running = false;
+    pthread_mutex_unlock(&g_pool_m);
 }
 // A warm context from the pool, or nullptr (none left and the thread has finished).
 Ctx* pool_take() {
-    std::unique_lock<std::mutex> g(g_pool_m);
-    g_pool_cv.wait(g, [] { return !g_pool.empty() || !g_pre_running; });
-    if (g_pool.empty()) return nullptr;
-    Ctx* c = g_pool.back();
-    g_pool.pop_back();
+    pthread_mutex_lock(&g_pool_m);
+    while (g_pool_n == 0 && g_pre_running) pthread_cond_wait(&g_pool_cv, &g_pool_m);
+    Ctx* c = g_pool_n ? g_pool[--g_pool_n] : nullptr;
+    pthread_mutex_unlock(&g_pool_m);
     return c;
 }
 

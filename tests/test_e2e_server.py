@@ -110,14 +110,17 @@ def battery2(exe, tmp, env=None, settle=0.0):
     srv = Server(exe, tmp, {"MAXSTORAGECAP": 1000000, "MAXFILECOUNT": 10, "WORKERPOOLSIZE": 4,
                             "REPLACEMENTALGO": 1}, env, settle)
     b = lambda n: os.path.join(files, "bigfiles", n)
+    t0 = time.perf_counter()
     try:
         srv.client("-W", f"{b('big2')},{b('randbig')}")
         time.sleep(1.1)   # the LRU clock has 1-second resolution (tests/test2.sh:18)
         srv.client("-r", b("big2"), "-d", os.path.join(tmp, "readback"))
         srv.client("-W", b("big4"), "-D", os.path.join(tmp, "evicted1"))
     finally:
+        wall = time.perf_counter() - t0 - 1.1   # from the socket's appearance (+ settle), less the sleep
         text = srv.stop()
-    return _max_storage(text), _returned(os.path.join(tmp, "evicted1")), _returned(os.path.join(tmp, "readback"))
+    return (_max_storage(text), _returned(os.path.join(tmp, "evicted1")), _returned(os.path.join(tmp, "readback")),
+            wall)
 
 
 def _src(name):
@@ -137,7 +140,7 @@ def _check_battery1(res):
 
 
 def _check_battery2(res):
-    stat, ev, rb = res
+    stat, ev, rb, _ = res
     assert stat == 942363
     assert list(ev) == ["randbig"] and ev["randbig"] == [_src("randbig")]
     assert rb["big2"] == [bytes(360000)]

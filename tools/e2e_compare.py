@@ -103,10 +103,9 @@ def run(exe, env, reps):
                 E._check_battery1(r1)
                 out["battery1%s_s" % key].append(round(r1[3], 4))
             with tempfile.TemporaryDirectory() as tmp:
-                t0 = time.perf_counter()
-                E._check_battery2(E.battery2(exe, os.path.join(tmp, "b2"), env, settle))
-                # less the LRU-clock sleep and the settle time
-                out["battery2%s_s" % key].append(round(time.perf_counter() - t0 - 1.1 - settle, 4))
+                r2 = E.battery2(exe, os.path.join(tmp, "b2"), env, settle)
+                E._check_battery2(r2)
+                out["battery2%s_s" % key].append(round(r2[3], 4))   # from the socket's appearance, less the sleep
         with tempfile.TemporaryDirectory() as tmp:
             cold, hot = battery3(exe, tmp, env)
             out["battery3_cold_s"].append(round(cold, 4))

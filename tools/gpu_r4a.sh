@@ -8,6 +8,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 hostname > $O/host.txt
 fatal() { case $1 in 124|134|137|139) exit $1;; esac; }
+timeout -k 10 60 $R/build/sync_probe > $O/sync_probe.txt 2>&1
+rc=$?; echo "sync_probe rc=$rc" >> $O/status; fatal $rc
 timeout -k 10 60 $R/build/store_probe > $O/store_probe.txt 2>&1
 rc=$?; echo "store_probe rc=$rc" >> $O/status; fatal $rc
 timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -q -rA --timeout 120 --timeout-method thread > $O/pytest.log 2>&1

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-4 second GPU pass: the -m gpu suite (e2e last), launch-timing modes, e2e side by side,
+# the call rate and the completion-latency probe.   usage: bash tools/gpu_r4b.sh TAG
+set -o pipefail
+TAG=${1:-r4b}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+hostname > $O/host.txt
+fatal() { case $1 in 124|134|137|139) exit $1;; esac; }
+timeout -k 10 700 python -u -m pytest $R/tests -m gpu -q -rA --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/status; fatal $rc
+timeout -k 10 300 python -u $R/tools/launch_modes.py > $O/launch_modes.json 2> $O/launch_modes.err
+rc=$?; echo "launch_modes rc=$rc" >> $O/status; fatal $rc
+timeout -k 10 300 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
+rc=$?; echo "e2e_compare rc=$rc" >> $O/status; fatal $rc
+for T in 1 8 16; do
+  timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
+  rc=$?; echo "callrate $T rc=$rc" >> $O/status; fatal $rc
+done
+exit 0
