@@ -33,6 +33,16 @@ constexpr u32 kCoopMaxWaves = 8;
 
 __device__ __forceinline__ u32 coop_wave() { return uniform(threadIdx.x / kWave); }
 
+// Completion-flag launches (put_status): every wave that stored output releases its stores before
+// the barrier behind which thread 0 stores the status.  All waves still running reach it (the
+// waves without a tile ended before the first barrier).
+__device__ __forceinline__ void coop_release(u32 flags) {
+    if (flags & kLaunchFlag) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+    }
+}
+
 // ================================================================ ENCODE
 // kW waves; 1024-byte tiles (enc_tile<true> form), so buffers of up to 1024 kW bytes are coop.
 template <u32 kW>
@@ -63,7 +73,7 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
     if (bad) {
         if (threadIdx.x == 0) {
             out_len[b] = 0;
-            if (status) status[b] = bad;
+            put_status(status, b, bad, wt);
         }
         return;
     }
@@ -74,7 +84,7 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
     const u32 ntiles = enc_ntiles_for(U);
     if (ntiles > kW) {   // too long for one round: wave 0 walks it like encode_kernel
         if (wid != 0u) return;
-        EncState st{0u, 0u, 0u, 0u, 0u, wt != 0u, {}};
+        EncState st{0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
         if (U <= 16384u)   // rle_kernels.hip kEncSmall
             walk_tiles<kEncStep, true>(rsi, 0u, enc_ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
                 return enc_tile<true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc);
@@ -86,7 +96,7 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
         if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
         if (lane == 0) {
             out_len[b] = st.out_pos;
-            if (status) status[b] = RLE_STATUS_OK;
+            put_status(status, b, RLE_STATUS_OK, wt);
         }
         return;
     }
@@ -160,11 +170,12 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
     // store: whole 16-byte chunks, then the final partial chunk byte by byte (nothing past C)
     const u32 nthr = kWave * nact, t = threadIdx.x, nfull = total >> 4;
     for (u32 c = t; c < nfull; c += nthr)
-        vstore(rso, 16u * c, *reinterpret_cast<const u32x4*>(stage + 16u + 16u * c), wt != 0u);
+        vstore(rso, 16u * c, *reinterpret_cast<const u32x4*>(stage + 16u + 16u * c), (wt & kLaunchWt) != 0u);
     if (t < (total & 15u)) dst[16u * nfull + t] = stage[16u + 16u * nfull + t];
+    coop_release(wt);
     if (t == 0) {
         out_len[b] = total;
-        if (status) status[b] = RLE_STATUS_OK;
+        put_status(status, b, RLE_STATUS_OK, wt);
     }
 }
 
@@ -201,7 +212,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
     if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
     if (bad) {
-        if (threadIdx.x == 0 && status) status[b] = bad;
+        if (threadIdx.x == 0) put_status(status, b, bad, wt);
         return;
     }
     const u32 C = (u32)C64, U = (u32)U64;
@@ -215,7 +226,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
         walk_prime(rsi, 0u, ntiles, lane, slots);
         for (u32 k = lane; k < kDecStage / 16u; k += kWave) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
         wave_lds_sync();
-        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, wt != 0u, {}};
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
         const bool serial = walk_tiles(
             rsi, 0u, ntiles, lane, slots,
             [&](u32 t, const uint8_t* cs, const Refill& nx) { return dec_tile(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc); },
@@ -226,7 +237,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
             dec_finish(st, U, lane, stage, rso, dst);
             stat = dec_tiled_status(st, U);
         }
-        if (lane == 0 && status) status[b] = stat;
+        if (lane == 0) put_status(status, b, stat, wt);
         return;
     }
     const u32 nact = ntiles ? ntiles : 1u;
@@ -284,7 +295,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     if (serial || total > U) {   // not encoder output: the exact serial decoder (dec_tile declines)
         if (wid == 0u) {
             const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage);
-            if (lane == 0 && status) status[b] = stat;
+            if (lane == 0) put_status(status, b, stat, wt);
         }
         return;
     }
@@ -314,13 +325,14 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
                 ob[k] = (fv[k] & m) | (tv & ~m);
             }
             if (16u * q + 16u <= U) {
-                vstore(rso, 16u * q, u32x4{ob[0], ob[1], ob[2], ob[3]}, wt != 0u);
+                vstore(rso, 16u * q, u32x4{ob[0], ob[1], ob[2], ob[3]}, (wt & kLaunchWt) != 0u);
             } else {
                 for (u32 j = 0; 16u * q + j < U; ++j) dst[16u * q + j] = (uint8_t)(ob[j >> 2] >> (8u * (j & 3u)));
             }
         }
     }
-    if (threadIdx.x == 0 && status) status[b] = total < U ? RLE_STATUS_SHORT : RLE_STATUS_OK;
+    coop_release(wt);
+    if (threadIdx.x == 0) put_status(status, b, total < U ? RLE_STATUS_SHORT : RLE_STATUS_OK, wt);
 }
 
 }  // namespace rle
@@ -382,12 +394,12 @@ bool coop_admits(uint32_t threads, uint32_t n) {
 // qualify (the caller then uses the one-wave kernels), < 0 on a launch error.
 extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
                                       const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
-                                      uint64_t max_len, void* stream) {
+                                      uint64_t max_len, uint32_t flags, void* stream) {
     if (max_len > rle::kEncStep * rle::kCoopMaxWaves || max_len <= rle::kEncStep) return 0;
     const uint32_t tiles = (uint32_t)((max_len + rle::kEncStep - 1) / rle::kEncStep);
     if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
     const hipStream_t s = (hipStream_t)stream;
-    const uint32_t wt = coop_store_policy(n);
+    const uint32_t wt = coop_store_policy(n) | flags;
     const dim3 g(n);
 #define RLE_ENC_COOP(W)                                                                                         \
     do {                                                                                                        \
@@ -407,14 +419,14 @@ extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off
 extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
                                       const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap,
                                       uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint64_t max_out_len,
-                                      void* stream) {
+                                      uint32_t flags, void* stream) {
     if (max_in_len > (uint64_t)rle::kTileStep * rle::kCoopMaxWaves || max_in_len <= rle::kTileStep ||
         max_out_len > 16384u)
         return 0;
     const uint32_t tiles = (uint32_t)((max_in_len + rle::kTileStep - 1) / rle::kTileStep);
     if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
     const hipStream_t s = (hipStream_t)stream;
-    const uint32_t wt = coop_store_policy(n);
+    const uint32_t wt = coop_store_policy(n) | flags;
     const dim3 g(n);
 #define RLE_DEC_COOP(W, UM)                                                                                      \
     do {                                                                                                         \

@@ -231,6 +231,23 @@ __device__ __forceinline__ void vm_wait(u32 n) {
 #undef RLE_VMW
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Launch flags, the kernels' `wt` argument: bit 0 write-through output stores (vstore), bit 1 the
+// status word is the caller's completion flag (include/rle_mi355x.h RLE_LAUNCH_STATUS_FLAG): every
+// earlier store of the wave is released at system scope (L2 write-back + store acknowledgement)
+// before the status store, so a host polling the status in mapped memory may then read the output.
+// A store acknowledgement alone is not enough: without the L2 write-back the host read stale output
+// words (tools/probes/sync_probe.hip, profiles/r4a_sync_probe.txt).
+constexpr u32 kLaunchWt = 1u, kLaunchFlag = 2u;
+__device__ __forceinline__ void put_status(uint32_t* status, u32 b, u32 v, u32 flags) {
+    if (!status) return;
+    if (flags & kLaunchFlag) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
+        __hip_atomic_store(status + b, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        status[b] = v;
+    }
+}
+
 // Tiles overlap: tile t is input [1008 t, 1008 t + 1024); lanes 0..62 own its first 1008 bytes
 // and lane 63 holds the next tile's first 16 bytes (the lookahead of lane 62).  Each tile is one
 // LDS-DMA into one of two slots.  A step reads its slot once (one ds_read_b128 per lane) and then

@@ -112,6 +112,11 @@ bool g_zerocopy = true;
 bool g_coalesce = false;   // concurrent zero-copy calls join one launch (submit); RLE_MI355X_COALESCE=1: on
 #endif
 size_t g_presize = 1u << 20;   // staging allocated with each thread context (presize); RLE_MI355X_PRESIZE
+// Zero-copy calls learn of their completion from the status word the kernel stores last, behind a
+// system-scope release of its output (RLE_LAUNCH_STATUS_FLAG), by polling it in the mapped buffer
+// instead of hipStreamSynchronize (profiles/r4a_sync_probe.txt: 11.7 against 16.2 us per 4 KiB
+// launch).  RLE_MI355X_POLL=0: synchronize instead.
+bool g_poll = true;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 
 // Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
@@ -151,6 +156,7 @@ struct Ctx {
     uint8_t* d_bm = nullptr;  size_t d_bm_cap = 0;
     uint8_t* h_cw = nullptr;                         // mapped launch words of combined launches (submit)
     uint8_t* d_cw = nullptr;
+    uint32_t polled = 0;                             // polled launches since the last stream synchronize
 };
 // h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
 //   decode [in_off, in_len, out_off, out_len, out_cap, status], encode [in_off, in_len, out_off,
@@ -204,6 +210,7 @@ void init_once() {
     if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
+    if (const char* e = getenv("RLE_MI355X_POLL")) g_poll = strcmp(e, "0") != 0;
 #if RLE_VARIANTS
     if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
 #endif
@@ -390,6 +397,15 @@ void grow_dev(uint8_t*& p, size_t& cap, size_t need) {
 
 namespace {
 
+// An encode whose status is not OK has no trustworthy output (RLE_STATUS_INTERNAL: the segmented
+// kernels' carry wait ran out; never expected): the call fails loudly rather than return it.
+void check_encode_status(uint32_t st) {
+    if (st != RLE_STATUS_OK) {
+        fprintf(stderr, "librle_mi355x: RLEcompress: encode status 0x%x\n", st);
+        abort();
+    }
+}
+
 // Queues on c->s the encode of n device bytes at d_src (16-byte aligned) into c->d_out, the D2H of
 // C into h_meta[kMetaEnc + 3] and, up to kOneTripBytes, of the worst-case output into h_out (one
 // stream sync per call).  Returns whether the output travels with its size.
@@ -407,7 +423,7 @@ bool queue_encode(Ctx* c, const uint8_t* d_src, size_t n) {
                                                       c->d_ws, c->d_ws_cap, c->s)
                         : rle_encode_batch_device_sized(d_src, dm + 0, dm + 1, c->d_out, dm + 2, dm + 3, d_status, 1, n, c->s);
     if (erc != RLE_OK) die("encode launch", hipGetLastError());
-    check(hipMemcpyAsync(hm + 3, dm + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
+    check(hipMemcpyAsync(hm + 3, dm + 3, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s), "D2H(meta)");
     const bool one_trip = n <= kOneTripBytes;
     if (one_trip) {
         grow_host(c->h_out, c->h_out_cap, maxC);
@@ -420,6 +436,7 @@ bool queue_encode(Ctx* c, const uint8_t* d_src, size_t n) {
 // and returns C.
 size_t fetch_encoded(Ctx* c, bool one_trip, size_t from) {
     const size_t C = c->h_meta[kMetaEnc + 3];
+    check_encode_status((uint32_t)c->h_meta[kMetaEnc + 5]);
     if (!one_trip && C > from) {
         grow_host(c->h_out, c->h_out_cap, C);
         check(hipMemcpyAsync(c->h_out + from, c->d_out + from, C - from, hipMemcpyDeviceToHost, c->s), "D2H");
@@ -704,6 +721,42 @@ void submit(Ctx* c, Req* r) {
 
 #endif  // RLE_VARIANTS
 
+// Launch flags and completion wait of a zero-copy call (g_poll): the status word in the mapped
+// buffer is preset to kPending and polled.  Past kPollNs of polling (a box under load, a kernel
+// fault) the stream is synchronized, which also reports a failed launch; every kPollSyncEvery polled
+// calls it is synchronized anyway, so the runtime's record of completed launches stays short.
+constexpr uint32_t kPending = 0xFFFFFFFFu;
+constexpr uint64_t kPollNs = 2000000;
+constexpr uint32_t kPollSyncEvery = 32;
+uint32_t zc_flags() { return g_poll ? RLE_LAUNCH_STATUS_FLAG : 0u; }
+uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
+    const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(status_word);
+    if (g_poll) {
+        uint64_t t0 = 0;
+        for (uint32_t i = 1;; ++i) {
+            const uint32_t v = __atomic_load_n(st, __ATOMIC_ACQUIRE);
+            if (v != kPending) {
+                if (++c->polled >= kPollSyncEvery) {
+                    c->polled = 0;
+                    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+                }
+                return v;
+            }
+            if ((i & 255u) == 0u) {
+                const uint64_t t = now_ns();
+                if (!t0) t0 = t;
+                else if (t - t0 > kPollNs) break;
+            }
+            __builtin_ia32_pause();
+        }
+    }
+    c->polled = 0;
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const uint32_t v = __atomic_load_n(st, __ATOMIC_ACQUIRE);
+    if (g_poll && v == kPending) die("status never stored", hipErrorUnknown);
+    return v;
+}
+
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, U);
@@ -718,12 +771,12 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
 #endif
     {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
-        hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0;
+        hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = kPending;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-        if (rle_encode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
-                                          reinterpret_cast<uint32_t*>(dw + 4), 1, U, c->s) != RLE_OK)
+        if (rle_encode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
+                                                reinterpret_cast<uint32_t*>(dw + 4), 1, U, zc_flags(), c->s) != RLE_OK)
             die("encode launch", hipGetLastError());
-        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        check_encode_status(zc_wait(c, hw + 4));
         C = hw[3];
     }
     *compressedSize = C;
@@ -749,13 +802,12 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
 #endif
     {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
-        hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
+        hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = kPending;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-        if (rle_decode_batch_device_sized(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
-                                          reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, c->s) != RLE_OK)
+        if (rle_decode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
+                                                reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, zc_flags(), c->s) != RLE_OK)
             die("decode launch", hipGetLastError());
-        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
-        st = (uint32_t)hw[5];
+        st = zc_wait(c, hw + 5);
     }
     memcpy(r, h + kZcOut, U);
     if (E) {
@@ -785,6 +837,7 @@ char* compress_small(Ctx* c, const char* data, size_t U, size_t* compressedSize)
     check(hipMemcpyAsync(c->h_out, c->d_out, Cr + kMetaBytes, hipMemcpyDeviceToHost, c->s), "D2H");
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
     const size_t C = reinterpret_cast<const uint64_t*>(c->h_out + Cr)[0];
+    check_encode_status((uint32_t)reinterpret_cast<const uint64_t*>(c->h_out + Cr)[1]);
     return make_block(c, nullptr, 0, 0, C, compressedSize);
 }
 
@@ -892,6 +945,7 @@ bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* a
     const uint64_t* hr = reinterpret_cast<const uint64_t*>(c->h_out + Er);
     const uint32_t st = (uint32_t)hr[2];
     const size_t rr = hr[3];
+    check_encode_status((uint32_t)hr[1]);
     const uint8_t ch = reinterpret_cast<const uint8_t*>(hr + 4)[15];
     const uint8_t* y = reinterpret_cast<const uint8_t*>(content);
     const size_t tok = rr == 1 ? 1 : 3;

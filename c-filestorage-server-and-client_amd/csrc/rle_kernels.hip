@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     if (bad) {
         if (lane == 0) {
             out_len[b] = 0;
-            if (status) status[b] = bad;
+            put_status(status, b, bad, wt);
         }
         return;
     }
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     const u32 U = (u32)U64;
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
-    EncState st{0u, 0u, 0u, 0u, 0u, wt != 0u, {}};
+    EncState st{0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
     const EncK kc = enc_k();
 #if RLE_STAMPS
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
     if (lane == 0) {
         out_len[b] = st.out_pos;
-        if (status) status[b] = RLE_STATUS_OK;
+        put_status(status, b, RLE_STATUS_OK, wt);
     }
     tl_mark(b, 10, lane);
     RLE_STAMP(st.sp, 7);   // finish
@@ -370,11 +370,11 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
 
     if (b < n) {
         if (bad) {
-            if (lane == 0 && status) status[b] = bad;
+            if (lane == 0) put_status(status, b, bad, wt);
             return;
         }
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, wt != 0u, {}};
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
         const DecK kc = dec_k();
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             atomicAdd(&g_stamps[kStampSegs], 1ull);
         }
 #endif
-        if (lane == 0 && status) status[b] = stat;
+        if (lane == 0) put_status(status, b, stat, wt);
         tl_mark(b, 10, lane);
     }
 }
@@ -518,6 +518,7 @@ __global__ void selftest_kernel(uint32_t* err) {
 
 // ================================================================ C-ABI launchers
 namespace {
+static_assert(RLE_LAUNCH_STATUS_FLAG == rle::kLaunchFlag, "launch flag bit (rle_device.h put_status)");
 constexpr uint32_t kMaxGrid = 1u << 30;
 // one buffer per wave, kWaves waves per workgroup, rounded up to whole rounds of the 8 XCDs
 // (rle::xcd_buffer); the kernels have no grid-stride loop, so n is bounded (kMaxGrid)
@@ -558,21 +559,30 @@ bool dec_order_enabled() {
 
 extern "C" size_t rle_max_compressed_size(size_t U) { return U + U / 2; }
 
-extern "C" int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
-                                       void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
-                                       uint32_t* d_status, uint32_t n, void* stream) {
+namespace {
+int encode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                  const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n, uint32_t flags,
+                  void* stream) {
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
     hipLaunchKernelGGL(rle::encode_kernel, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n,
-                       store_policy(n, true));
+                       store_policy(n, true) | flags);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
+}  // namespace
 
-extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
-                                       void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
-                                       const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n, void* stream) {
+extern "C" int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                       void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                                       uint32_t* d_status, uint32_t n, void* stream) {
+    return encode_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, 0u, stream);
+}
+
+namespace {
+int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                  const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap, uint32_t* d_status,
+                  uint32_t n, uint32_t flags, void* stream) {
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
@@ -597,44 +607,69 @@ extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_of
                                                                     : rle::decode_kernel<rle::kDecChunks>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
-                       d_status, n, store_policy(n, false), (const uint32_t*)order);
+                       d_status, n, store_policy(n, false) | flags, (const uint32_t*)order);
     if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
+}  // namespace
+
+extern "C" int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                       void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                                       const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n, void* stream) {
+    return decode_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n, 0u, stream);
 }
 
 // Cooperative small-buffer kernels (rle_coop.hip): 1 if launched, 0 if the batch does not qualify.
 extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
                                       const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
-                                      uint64_t max_len, void* stream);
+                                      uint64_t max_len, uint32_t flags, void* stream);
 extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
                                       const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap,
                                       uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint64_t max_out_len,
-                                      void* stream);
+                                      uint32_t flags, void* stream);
+
+extern "C" int rle_encode_batch_device_sized_flags(const void* d_in, const uint64_t* d_in_off,
+                                                   const uint64_t* d_in_len, void* d_out, const uint64_t* d_out_off,
+                                                   uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
+                                                   uint64_t max_in_len, uint32_t flags, void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
+    if (n > kMaxGrid || (flags & ~(uint32_t)RLE_LAUNCH_STATUS_FLAG) || ((flags & RLE_LAUNCH_STATUS_FLAG) && !d_status))
+        return RLE_E_INVAL;
+    const int c = rle_encode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, max_in_len,
+                                         flags, stream);
+    if (c != 0) return c > 0 ? RLE_OK : c;
+    return encode_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, flags, stream);
+}
 
 extern "C" int rle_encode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                              void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
                                              uint32_t* d_status, uint32_t n, uint64_t max_in_len, void* stream) {
+    return rle_encode_batch_device_sized_flags(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n,
+                                               max_in_len, 0u, stream);
+}
+
+extern "C" int rle_decode_batch_device_sized_flags(const void* d_in, const uint64_t* d_in_off,
+                                                   const uint64_t* d_in_len, void* d_out, const uint64_t* d_out_off,
+                                                   const uint64_t* d_out_len, const uint64_t* d_out_cap,
+                                                   uint32_t* d_status, uint32_t n, uint64_t max_in_len,
+                                                   uint64_t max_out_len, uint32_t flags, void* stream) {
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
-    if (n > kMaxGrid) return RLE_E_INVAL;
-    const int c = rle_encode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, max_in_len,
-                                         stream);
+    if (n > kMaxGrid || (flags & ~(uint32_t)RLE_LAUNCH_STATUS_FLAG) || ((flags & RLE_LAUNCH_STATUS_FLAG) && !d_status))
+        return RLE_E_INVAL;
+    const int c = rle_decode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n,
+                                         max_in_len, max_out_len, flags, stream);
     if (c != 0) return c > 0 ? RLE_OK : c;
-    return rle_encode_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_status, n, stream);
+    return decode_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n, flags, stream);
 }
 
 extern "C" int rle_decode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                              void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
                                              const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
                                              uint64_t max_in_len, uint64_t max_out_len, void* stream) {
-    if (n == 0) return RLE_OK;
-    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
-    if (n > kMaxGrid) return RLE_E_INVAL;
-    const int c = rle_decode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n,
-                                         max_in_len, max_out_len, stream);
-    if (c != 0) return c > 0 ? RLE_OK : c;
-    return rle_decode_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n,
-                                   stream);
+    return rle_decode_batch_device_sized_flags(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap,
+                                               d_status, n, max_in_len, max_out_len, 0u, stream);
 }
 
 extern "C" int rle_gen_synthetic_device(void* d_out, const uint64_t* d_off, const uint64_t* d_len,

@@ -24,6 +24,8 @@ RLE_STATUS_OVERFLOW = 1
 RLE_STATUS_MISALIGNED = 2
 RLE_STATUS_SERIAL = 0x100
 RLE_STATUS_SHORT = 0x400
+RLE_STATUS_INTERNAL = 0x800
+RLE_LAUNCH_STATUS_FLAG = 2
 
 _u64p = ctypes.c_void_p
 _lib = None
@@ -65,6 +67,10 @@ def lib():
     L.rle_encode_batch_device_sized.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u64, vp]
     L.rle_decode_batch_device_sized.restype = ctypes.c_int
     L.rle_decode_batch_device_sized.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u64, u64, vp]
+    L.rle_encode_batch_device_sized_flags.restype = ctypes.c_int
+    L.rle_encode_batch_device_sized_flags.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u64, u32, vp]
+    L.rle_decode_batch_device_sized_flags.restype = ctypes.c_int
+    L.rle_decode_batch_device_sized_flags.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u64, u64, u32, vp]
     L.rle_seg_workspace_bytes.restype = sz
     L.rle_seg_workspace_bytes.argtypes = [u32, ctypes.c_uint64]
     L.rle_encode_batch_device_seg.restype = ctypes.c_int
@@ -197,12 +203,16 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None, max_len=None):
+def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None, max_len=None, flags=0):
     """Batched encode on device tensors (uint8 data; int64 offsets/lengths; int32 status).  With
     max_len (>= every in_len) the sized entry point runs, which takes the cooperative kernels for
-    batches of small buffers."""
+    batches of small buffers; flags (RLE_LAUNCH_STATUS_FLAG) selects the *_sized_flags form."""
     n = in_off.numel()
-    if max_len is None:
+    if flags:
+        rc = lib().rle_encode_batch_device_sized_flags(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out),
+                                                       _ptr(out_off), _ptr(out_len), _ptr(status), n,
+                                                       int(max_len), int(flags), _stream_ptr(stream))
+    elif max_len is None:
         rc = lib().rle_encode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
                                            _ptr(out_len), _ptr(status), n, _stream_ptr(stream))
     else:
@@ -213,11 +223,17 @@ def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, str
 
 
 def decode_batch(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, status=None, stream=None,
-                 max_in_len=None, max_out_len=None):
+                 max_in_len=None, max_out_len=None, flags=0):
     """Batched decode on device tensors.  With max_in_len / max_out_len (>= every in_len / out_len)
-    the sized entry point runs (cooperative kernels for batches of small buffers)."""
+    the sized entry point runs (cooperative kernels for batches of small buffers); flags
+    (RLE_LAUNCH_STATUS_FLAG) selects the *_sized_flags form."""
     n = in_off.numel()
-    if max_in_len is None or max_out_len is None:
+    if flags:
+        rc = lib().rle_decode_batch_device_sized_flags(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out),
+                                                       _ptr(out_off), _ptr(out_len), _ptr(out_cap), _ptr(status), n,
+                                                       int(max_in_len), int(max_out_len), int(flags),
+                                                       _stream_ptr(stream))
+    elif max_in_len is None or max_out_len is None:
         rc = lib().rle_decode_batch_device(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
                                            _ptr(out_len), _ptr(out_cap), _ptr(status), n, _stream_ptr(stream))
     else:

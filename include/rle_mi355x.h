@@ -83,6 +83,24 @@ int rle_decode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, co
                                   const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
                                   uint64_t max_in_len, uint64_t max_out_len, void* stream);
 
+/* The sized launches with launch flags.  RLE_LAUNCH_STATUS_FLAG (needs d_status): each buffer's
+ * status word is stored last, behind a system-scope release of every output byte and d_out_len
+ * word of that buffer, so a host that placed d_out / d_status in mapped pinned memory
+ * (hipHostMallocMapped) and preset the status words to a value no status takes (e.g. 0xFFFFFFFF)
+ * can poll them instead of synchronizing the stream: once a status word changes, the buffer's
+ * output is readable from the host.  The drop-in's small zero-copy calls work this way (saves
+ * ~4.5 us per call against hipStreamSynchronize, profiles/r4a_sync_probe.txt).  Other flag bits:
+ * RLE_E_INVAL. */
+#define RLE_LAUNCH_STATUS_FLAG 2u
+int rle_encode_batch_device_sized_flags(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                        void* d_out, const uint64_t* d_out_off, uint64_t* d_out_len,
+                                        uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint32_t flags,
+                                        void* stream);
+int rle_decode_batch_device_sized_flags(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                        void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                                        const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n,
+                                        uint64_t max_in_len, uint64_t max_out_len, uint32_t flags, void* stream);
+
 /* Synthetic batch generator: xorshift64 (13,7,17), state seed
  * 0x9E3779B97F4A7C15 + index, one step per byte; kind 0 zero, 1 random, 2 runs50,
  * 3 runs90, 4 pairs.  d_kind / d_index may be NULL (kind 1, index = i). */

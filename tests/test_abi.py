@@ -154,3 +154,16 @@ def test_dist_scan_workspace_is_the_callers():
     fake = ctypes.c_void_p(0x1000)   # never dereferenced: the call must fail on the workspace check
     assert L.rle_dist_offsets_device(fake, 8, 131072, fake, None, 0, None) == -1
     assert L.rle_dist_offsets_device(fake, 8, 131072, fake, fake, w - 8, None) == -1
+
+
+def test_launch_flags_are_validated_before_any_launch():
+    """rle_*_batch_device_sized_flags (include/rle_mi355x.h): only RLE_LAUNCH_STATUS_FLAG is a known
+    bit, and it needs a status array (the completion words); both are refused on the host."""
+    L = R.lib()
+    fake = ctypes.c_void_p(0x1000)   # never dereferenced: every call below fails on its arguments
+    for flags, st in ((1, fake), (4, fake), (R.RLE_LAUNCH_STATUS_FLAG | 8, fake), (R.RLE_LAUNCH_STATUS_FLAG, None)):
+        assert L.rle_encode_batch_device_sized_flags(fake, fake, fake, fake, fake, fake, st, 1, 4096, flags, None) == -1
+        assert L.rle_decode_batch_device_sized_flags(fake, fake, fake, fake, fake, fake, None, st, 1, 4096, 4096,
+                                                     flags, None) == -1
+    # n == 0 is a no-op whatever the pointers
+    assert L.rle_encode_batch_device_sized_flags(None, None, None, None, None, None, None, 0, 0, 2, None) == 0

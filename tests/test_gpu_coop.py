@@ -108,3 +108,34 @@ def test_hints_smaller_than_buffers_fall_back():
     xs = [O.gen(i % 5, 300 + i, s) for i, s in enumerate([3000, 9000, 20000, 70000, 1500, 100, 4096, 16385])]
     coop_parity(xs, enc_hint=2048, dec_hints=(2016, 4096))
     coop_parity(xs, enc_hint=8192, dec_hints=(8064, 16384))
+
+
+@pytest.mark.parametrize("coop", [1, 0])
+def test_completion_flag_launches_same_bytes(coop):
+    """RLE_LAUNCH_STATUS_FLAG (include/rle_mi355x.h, the drop-in's polled small calls): the status is
+    stored last behind a system-scope release; output, sizes and status are the same as without it,
+    in the cooperative kernels (multi-wave release before the barrier) and the one-wave kernels,
+    including their bad-slot, one-wave-fallback, short and serial exits."""
+    import rle_mi355x as R
+    R.set_coop_mode(coop)
+    sizes = [0, 1, 17, 1008, 1009, 2049, 4096, 5000, 8192, 12000, 16384]
+    xs = [O.gen(k % 5, 31 * k + 7, s) for k, s in enumerate(sizes)]
+    refs = [O.encode(x) for x in xs]
+    mx = max(len(x) for x in xs)
+    for hint in (mx, 4096):   # 4096: the longer buffers take the workgroup's one-wave fallback
+        ys, st = gpu_encode(xs, max_len=hint, flags=R.RLE_LAUNCH_STATUS_FLAG)
+        assert ys == refs and (st == 0).all(), st
+    streams = list(refs) + [b"aa:" + refs[4], b"abc", b"xx9" * 300]
+    us = [len(x) for x in xs] + [len(xs[4]), 5, 3000]
+    caps = list(us)
+    caps[len(xs)] += 64
+    mi = max(len(s) for s in streams)
+    for hints in ((mi, max(us)), (2016, 4096)):
+        got, st = gpu_decode(streams, us, caps, max_in_len=hints[0], max_out_len=hints[1],
+                             flags=R.RLE_LAUNCH_STATUS_FLAG)
+        ref, rst = gpu_decode(streams, us, caps, max_in_len=hints[0], max_out_len=hints[1])
+        assert got == ref and (st == rst).all(), (st, rst)
+        for i in range(len(xs)):
+            assert got[i] == xs[i], i
+        assert st[len(xs)] & R.RLE_STATUS_SERIAL and st[len(xs) + 1] == R.RLE_STATUS_SHORT
+    R.set_coop_mode(1)

@@ -26,7 +26,7 @@ def _i64(vals):
     return torch.tensor(np.asarray(vals, dtype=np.int64), device=DEV)
 
 
-def gpu_encode(bufs, seg=False, max_len=None):
+def gpu_encode(bufs, seg=False, max_len=None, flags=0):
     """Encode a list of byte strings in ONE batched launch (seg: the segmented multi-wave form;
     max_len: the sized entry point with that hint, which picks the cooperative kernels for small
     buffers); returns (outputs, status)."""
@@ -42,7 +42,8 @@ def gpu_encode(bufs, seg=False, max_len=None):
     out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
     if max_len is not None:
-        R.encode_batch(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status, max_len=max_len)
+        R.encode_batch(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status, max_len=max_len,
+                       flags=flags)
     else:
         (R.encode_batch_seg if seg else R.encode_batch)(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs),
                                                         out_len, status)
@@ -58,7 +59,7 @@ def gpu_encode(bufs, seg=False, max_len=None):
     return res, status.cpu().numpy()
 
 
-def gpu_decode(streams, usizes, caps=None, poison=True, seg=False, max_in_len=None, max_out_len=None):
+def gpu_decode(streams, usizes, caps=None, poison=True, seg=False, max_in_len=None, max_out_len=None, flags=0):
     n = len(streams)
     caps = caps if caps is not None else list(usizes)
     in_offs, in_total = R.layout([len(s) for s in streams])
@@ -71,7 +72,7 @@ def gpu_decode(streams, usizes, caps=None, poison=True, seg=False, max_in_len=No
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
     if max_in_len is not None:
         R.decode_batch(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out, _i64(out_offs), _i64(usizes),
-                       _i64(caps), status, max_in_len=max_in_len, max_out_len=max_out_len)
+                       _i64(caps), status, max_in_len=max_in_len, max_out_len=max_out_len, flags=flags)
     else:
         (R.decode_batch_seg if seg else R.decode_batch)(d_in, _i64(in_offs), _i64([len(s) for s in streams]), d_out,
                                                         _i64(out_offs), _i64(usizes), _i64(caps), status)
