@@ -615,9 +615,13 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
         lateb |= late ? RLE_STATUS_INTERNAL : 0u;
         if (lane == 0) {
             publish(incl + g, make_uint4(c.lb1, c.off, lateb, 0u), sflag + g, kFlagIncl);
+            // the status words were cleared by the plan launch: a late segment ORs its bit in itself
+            // (a later segment may rebuild its state from raw summaries and not carry it), and the
+            // last segment ORs what it carries, so no bit is overwritten
+            if (late && status) atomicOr(status + b, RLE_STATUS_INTERNAL);
             if (g + 1u == s1) {   // the buffer's last segment: C and the status
                 out_len[b] = c.off;
-                if (status) status[b] = lateb ? lateb : RLE_STATUS_OK;
+                if (lateb && status) atomicOr(status + b, lateb);
             }
         }
         enc_seg_write(src, dst, U, p0, p1, rs, off, lane, slots, stage, elut);
@@ -716,9 +720,10 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
             lateb |= late ? RLE_STATUS_INTERNAL : 0u;
             if (lane == 0) {
                 publish(incl + g, make_uint4(c.lb1, c.off, lateb, 0u), sflag + g, kFlagIncl);
+                if (late && status) atomicOr(status + b, RLE_STATUS_INTERNAL);   // (as enc_seg_fused_kernel)
                 if (g + 1u == s1) {   // the buffer's last segment: C and the status
                     out_len[b] = c.off;
-                    if (status) status[b] = lateb ? lateb : RLE_STATUS_OK;
+                    if (lateb && status) atomicOr(status + b, lateb);
                 }
             }
             enc_seg_write<true>(src, dst, U, p0, p1, uniform(mine.x), uniform(mine.y), lane, region, stage, elut);
@@ -1315,9 +1320,9 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
 #if RLE_VARIANTS
-    if (seg_res()) {
+    if (seg_res()) {   // (the plan clears the status words: the segments OR into them)
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
-                           maxseg, w.ticket, nullptr);
+                           maxseg, w.ticket, d_status);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
         hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
@@ -1326,9 +1331,9 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
                            sb, w.summ, w.incl, w.sflag, w.ticket);
         return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
     }
-    if (seg_fused()) {
+    if (seg_fused()) {   // (the plan clears the status words: the segments OR into them)
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
-                           maxseg, w.ticket, nullptr);
+                           maxseg, w.ticket, d_status);
         hipLaunchKernelGGL(rle::enc_seg_fused_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ,
                            w.incl, w.sflag, w.ticket);

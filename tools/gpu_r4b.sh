@@ -14,8 +14,11 @@ timeout -k 10 300 python -u $R/tools/launch_modes.py > $O/launch_modes.json 2> $
 rc=$?; echo "launch_modes rc=$rc" >> $O/status; fatal $rc
 timeout -k 10 300 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
 rc=$?; echo "e2e_compare rc=$rc" >> $O/status; fatal $rc
-for T in 1 8 16; do
-  timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
-  rc=$?; echo "callrate $T rc=$rc" >> $O/status; fatal $rc
+for P in 1 0; do
+  for T in 1 8 16; do
+    echo "poll=$P threads=$T" >> $O/callrate.txt
+    RLE_MI355X_POLL=$P timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
+    rc=$?; echo "callrate poll=$P $T rc=$rc" >> $O/status; fatal $rc
+  done
 done
 exit 0
