@@ -1378,9 +1378,12 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
 // inside the tile loop).
 struct DecK {
     u32 K80, K7F, C1, C2;
+    u32 LM3;   // lane % 3 (dec_uniform_tile)
 };
 __device__ __forceinline__ DecK dec_k() {
-    return DecK{vconst(0x80808080u), vconst(0x7F7F7F7Fu), vconst(0x08040201u), vconst(0x80402010u)};
+    const u32 lane = threadIdx.x & (kWave - 1u);
+    return DecK{vconst(0x80808080u), vconst(0x7F7F7F7Fu), vconst(0x08040201u), vconst(0x80402010u),
+                lane - 3u * ((lane * 0xABu) >> 9)};
 }
 struct DecPrep {
     u32 w[4], g[4];
@@ -1744,9 +1747,9 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     return rounds + 1u;
 }
 
-// Single-value tile (dec_tile): ttot copies of v after the staged partial chunk.
-__device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st,
-                                             const DecPrep& pr) {
+// Single-value tile (dec_tile): ttot copies of v after the staged partial chunk.  The caller sets
+// the tile's exit state (st.d, st.prev).
+__device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st) {
     const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl = total >> 4;
     const u32 vv = rep4(v);
     // chunk 0: the staged positions [0, rel0) filled like a flush, then v (every lane computes it)
@@ -1786,9 +1789,53 @@ __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t*
     st.fillc = v;
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
+    return rounds;
+}
+__device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st,
+                                             const DecPrep& pr) {
+    const u32 rounds = dec_fill_run(v, ttot, lane, stage, rso, st);
     st.d = bfe(readlane(pr.incl, kOwnLanes - 1u), 8u * st.d, 8);
     st.prev = readlane(pr.w[3], kOwnLanes - 1u);
     return rounds;
+}
+
+// ---------------------------------------------------------------- uniform tiles (zero-filled data)
+// A whole tile (not the stream's or segment's last) whose owned tokens are all "v v 9" from its
+// entry offset d on -- long runs, zero-filled data -- decodes to 336 x 9 = 3024 copies of v and
+// leaves the entry offset unchanged (1008 = 3 x 336).  Position p of the tile holds '9' where
+// (p - d) mod 3 == 2, else v; with 16 l + 4 k = l + k (mod 3), dword k of lane l follows pattern
+// (l + k - d) mod 3.  Tested before the tile analysis (dec_prepare, dec_lengths: about 135 VALU
+// of the 266 a zero tile cost, profiles/r4a_sq_kinds.md): lane 0's first 8 bytes on the scalar
+// unit, then every owned byte and the lookahead bytes its last token reads (lane 63's first d) on
+// the vector unit, so other tiles pay a few scalar instructions.  Byte-identical to the general
+// path: the same tokens, each 3 bytes long (its first two bytes are equal) with count 9.
+#ifndef RLE_DEC_UNIFORM
+#define RLE_DEC_UNIFORM 1
+#endif
+constexpr u32 kUniformOut = 9u * (kTileStep / 3u);   // 3024
+__device__ __forceinline__ u32 uniform_pat(u32 m, u32 vv) {
+    return m == 0u ? ((vv & 0xFF00FFFFu) | 0x00390000u)
+                   : m == 1u ? ((vv & 0xFFFF00FFu) | 0x00003900u) : ((vv & 0x00FFFF00u) | 0x39000039u);
+}
+// lm3 = lane % 3.  Returns whether the tile is uniform; v = its byte.
+__device__ __forceinline__ bool dec_uniform_tile(const u32x4 cur, u32 lane, u32 lm3, u32 d, u32& v) {
+    const u32 w0 = readlane(cur.x, 0), w1 = readlane(cur.y, 0);
+    v = (w0 >> (8u * d)) & 0xFFu;
+    const u32 vv = v * 0x01010101u;
+    const u32 ms = d == 0u ? 0u : 3u - d;   // lane 0's dword-0 pattern
+    const u32 dm = ~lowmask(8u * d);        // lane 0: positions before d belong to the previous tile
+    if (((w0 ^ uniform_pat(ms, vv)) & dm) | (w1 ^ uniform_pat(ms == 2u ? 0u : ms + 1u, vv))) return false;
+    const u32 t = lm3 + 3u - d;
+    const u32 m0 = t >= 3u ? t - 3u : t;
+    const u32 P0 = uniform_pat(0u, vv), P1 = uniform_pat(1u, vv), P2 = uniform_pat(2u, vv);
+    const u32 pa = m0 == 0u ? P0 : m0 == 1u ? P1 : P2;
+    const u32 pb = m0 == 0u ? P1 : m0 == 1u ? P2 : P0;
+    const u32 pc = m0 == 0u ? P2 : m0 == 1u ? P0 : P1;
+    // lane 63 (lookahead): only its first d bytes (the last token's second byte and digit)
+    const u32 mx = lane == 0u ? dm : lane == kWave - 1u ? ~dm : ~0u;
+    const u32 myzw = lane == kWave - 1u ? 0u : ~0u;
+    const u32 diff = ((cur.x ^ pa) & mx) | (((cur.y ^ pb) | (cur.z ^ pc) | (cur.w ^ pa)) & myzw);
+    return !__builtin_amdgcn_ballot_w64(diff != 0u);
 }
 
 // kChunks: the staging's chunks per wave (kDecChunks unless a kernel picks its own).
@@ -1912,6 +1959,14 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
+    if (kFast && RLE_DEC_UNIFORM && !st.head && pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
+        u32 v;
+        if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
+            const u32 r = dec_fill_run(v, kUniformOut, lane, stage, rso, st);
+            st.prev = readlane(cur.w, kOwnLanes - 1u);   // (st.d unchanged)
+            return r;
+        }
+    }
     const DecPrep pr = dec_prepare(cur, pos, C, Co, lane, tbl, kc);
     return dec_tile_pr<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
 }

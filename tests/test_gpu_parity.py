@@ -405,3 +405,29 @@ def test_decode_ragged_batches_past_one_round(n):
         assert dec[i] == ref, i
     assert all(st[i] != 0x7777 and (st[i] & R.RLE_STATUS_SERIAL) for i in range(3, n, 1001))
     assert all(st[i] & ~R.RLE_STATUS_SHORT == 0 for i in range(n) if (i - 3) % 1001)
+
+
+@pytest.mark.parametrize("seg", [False, True])
+def test_uniform_tiles(seg):
+    """Long runs ("v v 9" tokens over whole tiles: the uniform-tile path of rle_device.h
+    dec_uniform_tile), every token phase at the tile edges (literal prefixes of 0..6 bytes), bytes
+    0x00 / '9' / 0x80 / 0xFF, runs that end anywhere in a tile, next to literals and other runs;
+    then streams the encoder never emits: decoded size past U (serial path) and '8' counts."""
+    xs = []
+    for pre in range(7):
+        for v in (0x00, 0x39, 0x80, 0xFF):
+            body = bytes([v]) * (9 * 400 * (1 + pre % 3) + pre)
+            xs.append(O.gen(1, pre, pre) + body + O.gen(1, 50 + pre, 37) + bytes([v ^ 1]) * (5000 + 13 * pre))
+    xs += [bytes(65536), bytes([0x39]) * 100003, O.gen(3, 9, 70000)]
+    ys, st = gpu_encode(xs, seg=seg)
+    assert (st == 0).all()
+    assert ys == [O.encode(x) for x in xs]
+    dec, st = gpu_decode(ys, [len(x) for x in xs], seg=seg)
+    assert (st == 0).all() and dec == xs
+    z = O.encode(bytes(40000))
+    streams = [z, z, b"\x00\x008" * 2000, b"\x07\x079" * 1500 + b"ab"]
+    us = [30000, 39999, 16000, 13502]
+    dec, st = gpu_decode(streams, us, poison=False, seg=seg)
+    for i in range(len(streams)):
+        ref, _ = O.decode(streams[i], us[i], us[i])
+        assert dec[i] == ref, i

@@ -10,6 +10,10 @@ hostname > $O/host.txt
 fatal() { case $1 in 124|134|137|139) exit $1;; esac; }
 timeout -k 10 700 python -u -m pytest $R/tests -m gpu -q -rA --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/status; fatal $rc
+timeout -k 10 300 python -u $R/tools/ab_events.py --workloads cfg1,dec64k,k64_zero,c4k_zero --reps 10 --rounds 5 > $O/ab.json 2> $O/ab.err
+rc=$?; echo "ab rc=$rc" >> $O/status; fatal $rc
+timeout -k 10 300 python -u $R/tools/ab_events.py --seg --workloads m1_zero,mixed --reps 5 --rounds 5 > $O/ab_seg.json 2> $O/ab_seg.err
+rc=$?; echo "ab_seg rc=$rc" >> $O/status; fatal $rc
 timeout -k 10 300 python -u $R/tools/launch_modes.py > $O/launch_modes.json 2> $O/launch_modes.err
 rc=$?; echo "launch_modes rc=$rc" >> $O/status; fatal $rc
 timeout -k 10 300 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
