@@ -23,6 +23,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -63,6 +65,31 @@ inline uint64_t now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+
+// RLE_MI355X_TRACE=<path> (diagnostics of the e2e batteries): one record per drop-in
+// call -- the entry point, its sizes, start and duration, the calling thread and the time it spent
+// getting its context (pool wait or creation) -- written to <path> at exit.  Off: one branch per call.
+struct TraceRec {
+    char op;
+    uint32_t tid;
+    uint64_t a, b, c, t0, dt, ctx_ns;
+};
+constexpr uint32_t kTraceMax = 1u << 16;
+TraceRec* g_trace = nullptr;
+std::atomic<uint32_t> g_trace_n{0};
+thread_local uint64_t t_ctx_ns = 0;
+struct TraceScope {
+    char op;
+    uint64_t a, b, c, t0;
+    TraceScope(char o, uint64_t x, uint64_t y, uint64_t z) : op(o), a(x), b(y), c(z), t0(g_trace ? now_ns() : 0) {
+        t_ctx_ns = 0;
+    }
+    ~TraceScope() {
+        if (!g_trace) return;
+        const uint32_t i = g_trace_n.fetch_add(1, std::memory_order_relaxed);
+        if (i < kTraceMax) g_trace[i] = TraceRec{op, (uint32_t)syscall(SYS_gettid), a, b, c, t0, now_ns() - t0, t_ctx_ns};
+    }
+};
 
 [[noreturn]] void die(const char* what, hipError_t e) {
     fprintf(stderr, "librle_mi355x: %s failed: %s\n", what, hipGetErrorString(e));
@@ -315,6 +342,8 @@ void preinit_join() {
 }
 void preinit_exit() { preinit_join(); }
 __attribute__((constructor)) void preinit_start() {
+    if (const char* t = getenv("RLE_MI355X_TRACE"))
+        if (*t) g_trace = static_cast<TraceRec*>(calloc(kTraceMax, sizeof(TraceRec)));
     const char* e = getenv("RLE_MI355X_PREINIT");
     if (e && atoi(e) <= 0) return;
     atexit(preinit_exit);
@@ -344,10 +373,12 @@ Ctx* ctx() {
         fprintf(stderr, "librle_mi355x: no HIP device is visible; the RLE codec runs on MI355X only\n");
         abort();
     }
+    const uint64_t t0 = g_trace ? now_ns() : 0;
     c = pool_take();
     if (c) check(hipSetDevice(c->dev), "hipSetDevice");
     else c = new_ctx((g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev));
     pthread_setspecific(g_key, c);
+    if (g_trace) t_ctx_ns = now_ns() - t0;
     return c;
 }
 
@@ -1005,6 +1036,7 @@ static char* compress_impl(char* data, size_t U, size_t* compressedSize) {
 // = ENOMEM) when an allocation fails, as the reference's calloc can (:10).
 extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize) {
     const size_t U = origSize;
+    TraceScope ts('c', U, 0, 0);
     if (U == 0 || too_big("RLEcompress", U)) {
         *compressedSize = 0;
         return U == 0 ? static_cast<char*>(calloc(16, 1)) : nullptr;
@@ -1067,6 +1099,7 @@ static void decompress_impl(char* data, size_t C, size_t U, size_t E, char* r) {
 // (errno = ENOMEM) when an allocation fails, as the reference's calloc can (:48).
 extern "C" char* RLEdecompress(char* data, size_t compressedSize, size_t uncompressedSize, size_t extraAllocation) {
     const size_t C = compressedSize, U = uncompressedSize, E = extraAllocation, total = U + E;
+    TraceScope ts('d', C, U, E);
     if (too_big("RLEdecompress", C) || too_big("RLEdecompress", U)) return nullptr;
     char* r = static_cast<char*>(malloc(total ? total : 1));
     if (!r) return nullptr;
@@ -1176,6 +1209,7 @@ static char* append_impl(char* content, size_t C, size_t U, const char* newConte
 extern "C" char* RLEappend(char* content, size_t contentSize, size_t uncompressedSize, const char* newContent,
                            size_t newContentLen, size_t* newCompressedSize) {
     const size_t C = contentSize, U = uncompressedSize, A = newContentLen;
+    TraceScope ts('a', C, U, A);
     // U == 0: the decode keeps nothing below U and whatever it writes into the extra region is
     // overwritten by the appended bytes (:767-770), so the result is encode(newContent)
     if (U == 0) return RLEcompress(const_cast<char*>(newContent), A, newCompressedSize);
@@ -1350,6 +1384,7 @@ int decompress_n_impl(size_t n, char* const* data, const size_t* compressedSize,
 // with the batch.
 extern "C" int RLEdecompressN(size_t n, char* const* data, const size_t* compressedSize,
                               const size_t* uncompressedSize, char* const* out) {
+    TraceScope ts('n', n, 0, 0);
     if (n == 0) return 0;
     if (!data || !compressedSize || !uncompressedSize || !out) {
         errno = EINVAL;
@@ -1392,6 +1427,18 @@ namespace {
 // (used to record the server's host<->device rate).
 struct StatsAtExit {
     ~StatsAtExit() {
+        if (g_trace) {
+            if (FILE* f = fopen(getenv("RLE_MI355X_TRACE"), "w")) {
+                const uint32_t n = std::min(g_trace_n.load(), kTraceMax);
+                for (uint32_t i = 0; i < n; ++i) {
+                    const TraceRec& t = g_trace[i];
+                    fprintf(f, "%c %u %llu %llu %llu %llu %llu %llu\n", t.op, t.tid, (unsigned long long)t.a,
+                            (unsigned long long)t.b, (unsigned long long)t.c, (unsigned long long)t.t0,
+                            (unsigned long long)t.dt, (unsigned long long)t.ctx_ns);
+                }
+                fclose(f);
+            }
+        }
         const char* path = getenv("RLE_MI355X_STATS");
         if (!path || !*path) return;
         rle_dropin_stats_t s;

@@ -18,6 +18,8 @@ timeout -k 10 300 python -u $R/tools/launch_modes.py > $O/launch_modes.json 2> $
 rc=$?; echo "launch_modes rc=$rc" >> $O/status; fatal $rc
 timeout -k 10 300 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
 rc=$?; echo "e2e_compare rc=$rc" >> $O/status; fatal $rc
+timeout -k 10 200 python -u $R/tools/e2e_trace.py > $O/e2e_trace.json 2> $O/e2e_trace.err
+rc=$?; echo "e2e_trace rc=$rc" >> $O/status; fatal $rc
 for P in 1 0; do
   for T in 1 8 16; do
     echo "poll=$P threads=$T" >> $O/callrate.txt
