@@ -45,14 +45,13 @@ __device__ __forceinline__ void coop_release(u32 flags) {
 
 // ================================================================ ENCODE
 // kW waves; 1024-byte tiles (enc_tile<true> form), so buffers of up to 1024 kW bytes are coop.
-template <u32 kW>
-__global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __restrict__ in,
-                                                             const uint64_t* __restrict__ in_off,
-                                                             const uint64_t* __restrict__ in_len,
-                                                             uint8_t* __restrict__ out,
-                                                             const uint64_t* __restrict__ out_off,
-                                                             uint64_t* __restrict__ out_len,
-                                                             uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+// One buffer (b: its index in out_len / status).  kU (the resident small-call service,
+// rle_service.hip, whose workgroup serves one buffer after another): no wave ends before the last
+// barrier -- the waves without a tile idle through the barriers -- and all of them share the stores.
+template <u32 kW, bool kU>
+__device__ __forceinline__ void enc_coop_body(const uint8_t* src, uint8_t* dst, uint64_t U64,
+                                              uint64_t* __restrict__ out_len, uint32_t* __restrict__ status, u32 b,
+                                              u32 wt) {
     constexpr u32 kUmax = kEncStep * kW;
     // output position r at byte 16 + r (chunk 0: guard of the non-starts' back-writes); +32: the
     // writes of positions past U land at the output end
@@ -63,11 +62,6 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
     __shared__ u32 xch[2 * kW];   // [0, kW) last run boundary per tile, [kW, 2kW) compressed size
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = coop_wave();
-    const u32 b = blockIdx.x;
-    if (b >= n) return;
-    const uint64_t U64 = in_len[b];
-    const uint8_t* src = in + in_off[b];
-    uint8_t* dst = out + out_off[b];
     u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
     if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
     if (bad) {
@@ -101,7 +95,7 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
         return;
     }
     const u32 nact = ntiles ? ntiles : 1u;   // waves with a tile (wave 0 also for U = 0)
-    if (wid >= nact) return;                 // ended waves do not hold up s_barrier
+    if (!kU && wid >= nact) return;          // ended waves do not hold up s_barrier
     const uint8_t* slot = slots + wid * kEncSlot;
     const bool act = wid < ntiles;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
@@ -168,7 +162,7 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
     }
     __syncthreads();
     // store: whole 16-byte chunks, then the final partial chunk byte by byte (nothing past C)
-    const u32 nthr = kWave * nact, t = threadIdx.x, nfull = total >> 4;
+    const u32 nthr = kWave * (kU ? kW : nact), t = threadIdx.x, nfull = total >> 4;
     for (u32 c = t; c < nfull; c += nthr)
         vstore(rso, 16u * c, *reinterpret_cast<const u32x4*>(stage + 16u + 16u * c), (wt & kLaunchWt) != 0u);
     if (t < (total & 15u)) dst[16u * nfull + t] = stage[16u + 16u * nfull + t];
@@ -178,18 +172,25 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
         put_status(status, b, RLE_STATUS_OK, wt);
     }
 }
-
-// ================================================================ DECODE
-// kW waves (tiles of 1008 bytes: dec_tile's geometry); buffers decoding to at most kUmax bytes.
-template <u32 kW, u32 kUmax>
-__global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __restrict__ in,
+template <u32 kW>
+__global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __restrict__ in,
                                                              const uint64_t* __restrict__ in_off,
                                                              const uint64_t* __restrict__ in_len,
                                                              uint8_t* __restrict__ out,
                                                              const uint64_t* __restrict__ out_off,
-                                                             const uint64_t* __restrict__ out_len,
-                                                             const uint64_t* __restrict__ out_cap,
+                                                             uint64_t* __restrict__ out_len,
                                                              uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+    const u32 b = blockIdx.x;
+    if (b >= n) return;
+    enc_coop_body<kW, false>(in + in_off[b], out + out_off[b], in_len[b], out_len, status, b, wt);
+}
+
+// ================================================================ DECODE
+// kW waves (tiles of 1008 bytes: dec_tile's geometry); buffers decoding to at most kUmax bytes.
+// One buffer (b: its index in status; kU as enc_coop_body).
+template <u32 kW, u32 kUmax, bool kU>
+__device__ __forceinline__ void dec_coop_body(const uint8_t* src, uint8_t* dst, uint64_t C64, uint64_t U64,
+                                              uint64_t cap, uint32_t* __restrict__ status, u32 b, u32 wt) {
     // decoded position r at u16 16 + r (dec_tile's staging, one for the whole buffer); the one-wave
     // fallback needs kDecStage
     constexpr u32 kStageC = 2u * (16u + kUmax + 32u);
@@ -202,13 +203,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     __shared__ u32 lastb[kChunks + 1];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = coop_wave();
-    const u32 b = blockIdx.x;
-    if (b >= n) return;
     for (u32 i = threadIdx.x; i < 256u; i += kWave * kW) tbl[i] = dec_entry_from(kDecTable.e[i]);
-    const uint64_t* capp = out_cap ? out_cap : out_len;
-    const uint64_t C64 = in_len[b], U64 = out_len[b], cap = capp[b];
-    const uint8_t* src = in + in_off[b];
-    uint8_t* dst = out + out_off[b];
     u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
     if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
     if (bad) {
@@ -241,14 +236,15 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
         return;
     }
     const u32 nact = ntiles ? ntiles : 1u;
-    if (wid >= nact) return;   // ended waves do not hold up s_barrier
+    if (!kU && wid >= nact) return;   // ended waves do not hold up s_barrier
+    const u32 nthr = kWave * (kU ? kW : nact);   // threads zeroing, filling and storing
     const uint8_t* slot = slots + wid * kSlot;
     const bool act = wid < ntiles;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
     if (act) dma_tile(rsi, kTileStep * wid + 16u * lane, uniform(lds_addr(slot)));
     // the staging positions this buffer can reach: [0, 16 + U + 17) u16
     const u32 nz = (2u * (16u + U + 17u) + 15u) / 16u;
-    for (u32 k = threadIdx.x; k < nz; k += kWave * nact) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
+    for (u32 k = threadIdx.x; k < nz; k += nthr) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     vm_drain();
     __syncthreads();   // tiles landed; table and zeroed staging visible
     DecPrep pr{};
@@ -304,7 +300,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     // output chunk q (bytes [16q, 16q + 16)) = staging chunk q + 1: decoded positions below total,
     // then the tail byte (zero unless the stream ends in an unbounded token); every chunk holds a
     // key, so the byte entering chunk q is chunk q - 1's last key (lastb, through LDS across waves)
-    const u32 nq = (U + 15u) >> 4, nthr = kWave * nact, tv = rep4(tail & 0xFFu);
+    const u32 nq = (U + 15u) >> 4, tv = rep4(tail & 0xFFu);
     for (u32 q0 = 0; q0 < nq; q0 += nthr) {
         const u32 q = q0 + threadIdx.x;
         u32x4 a, c;
@@ -333,6 +329,20 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     }
     coop_release(wt);
     if (threadIdx.x == 0) put_status(status, b, total < U ? RLE_STATUS_SHORT : RLE_STATUS_OK, wt);
+}
+template <u32 kW, u32 kUmax>
+__global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len,
+                                                             uint8_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ out_off,
+                                                             const uint64_t* __restrict__ out_len,
+                                                             const uint64_t* __restrict__ out_cap,
+                                                             uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+    const u32 b = blockIdx.x;
+    if (b >= n) return;
+    const uint64_t* capp = out_cap ? out_cap : out_len;
+    dec_coop_body<kW, kUmax, false>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
 }
 
 }  // namespace rle
