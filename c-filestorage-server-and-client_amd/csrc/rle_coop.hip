@@ -21,6 +21,7 @@
 // than its staging) is walked by wave 0 alone with the one-wave tile loop; streams the tiled path
 // declines take the exact serial decoder, as there.
 #include "rle_device.h"
+#include "rle_service.h"
 
 #include <stdlib.h>
 #include <string.h>
@@ -345,6 +346,92 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     dec_coop_body<kW, kUmax, false>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
 }
 
+// ================================================================ resident small-call service
+// (rle_service.h).  Wave 0 polls: lane s reads req[s] and claim[s]; the first pending slot this
+// workgroup claims (compare-and-swap of claim[s] from its last claimed sequence to the posted one)
+// is served by all kSvcWaves waves through the barrier-uniform codec bodies; every wave releases
+// its stores at system scope, and after a barrier thread 0 stores ack[s].  With nothing pending
+// anywhere for idle_ticks (the activity word: the latest claim of any workgroup), at life_ticks
+// after the launch, on the stop word, or after kSvcMaxPolls polls, the workgroup marks gone[g] and
+// ends.  The mailbox fields are read with system-scope atomic loads (vector loads that bypass the
+// caches; never the scalar cache).
+constexpr u32 kSvcNone = 0xFFFFFFFFu, kSvcExit = 0xFFFFFFFEu;
+constexpr u32 kSvcUmax = 16384;
+constexpr u32 kSvcMaxPolls = 1u << 24;
+__device__ __forceinline__ u32 svc_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t svc_ld64(const uint64_t* p) {
+    const uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return ((uint64_t)uniform((u32)(v >> 32)) << 32) | uniform((u32)v);
+}
+__global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcBox* box, uint32_t* __restrict__ claim,
+                                                              unsigned long long* __restrict__ activity, uint32_t gen,
+                                                              uint64_t idle_ticks, uint64_t life_ticks) {
+    __shared__ u32 sh[2];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = coop_wave();
+    const uint64_t t0 = wall_clock64();
+    for (u32 polls = 0;; ++polls) {
+        if (wid == 0u) {
+            const u32 r = svc_ld(&box->req[lane]);
+            const u32 c = __hip_atomic_load(&claim[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t pend = __builtin_amdgcn_ballot_w64(r != c);
+            u32 slot = kSvcNone, seq = 0u;
+            while (pend) {   // another workgroup may claim a slot first
+                const u32 sl = (u32)__builtin_ctzll(pend);
+                pend &= pend - 1ull;
+                const u32 want = readlane(c, sl), got = readlane(r, sl);
+                u32 old = 0u;
+                if (lane == 0u) old = atomicCAS(&claim[sl], want, got);
+                if (readlane(old, 0) == want) {
+                    slot = sl;
+                    seq = got;
+                    break;
+                }
+            }
+            const uint64_t now = wall_clock64();
+            if (slot != kSvcNone) {
+                if (lane == 0u) atomicMax(activity, (unsigned long long)now);
+            } else {
+                const uint64_t act = __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t since = now - (act > t0 ? act : t0);
+                if (svc_ld(&box->stop) || since > idle_ticks || now - t0 > life_ticks || polls > kSvcMaxPolls)
+                    slot = kSvcExit;
+            }
+            if (lane == 0u) {
+                sh[0] = slot;
+                sh[1] = seq;
+            }
+        }
+        __syncthreads();
+        const u32 slot = uniform(sh[0]), seq = uniform(sh[1]);
+        __syncthreads();   // (wave 0 rewrites sh at the next poll)
+        if (slot == kSvcExit) {
+            if (threadIdx.x == 0) __hip_atomic_store(&box->gone[blockIdx.x], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        if (slot == kSvcNone) {
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        SvcDesc* d = &box->desc[slot];
+        const u32 op = uniform(svc_ld(&d->op)), wt = uniform(svc_ld(&d->flags)) & kLaunchWt;
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(svc_ld64(&d->src));
+        uint8_t* dst = reinterpret_cast<uint8_t*>(svc_ld64(&d->dst));
+        const uint64_t in_len = svc_ld64(&d->in_len);
+        if (op == kSvcEncode) {
+            enc_coop_body<kSvcWaves, true>(src, dst, in_len, &d->res_len, &d->res_status, 0u, wt);
+        } else {
+            const uint64_t out_len = svc_ld64(&d->out_len), cap = svc_ld64(&d->cap);
+            dec_coop_body<kSvcWaves, kSvcUmax, true>(src, dst, in_len, out_len, cap, &d->res_status, 0u, wt);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's output, system scope
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&box->ack[slot], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace rle
 
 // ================================================================ C-ABI launchers
@@ -464,4 +551,16 @@ extern "C" int rle_mi355x_set_coop_mode(int mode) {
     if (mode < -1 || mode > 1) return RLE_E_INVAL;
     g_coop_mode.store(mode, std::memory_order_relaxed);
     return RLE_OK;
+}
+
+// The resident small-call service (rle_service.h; launched by the drop-in, csrc/rle_dropin.cpp
+// svc_ensure): kSvcGroups workgroups of kSvcWaves waves on the caller's stream.
+extern "C" int rle_service_launch(void* d_box, uint32_t* d_claim, unsigned long long* d_activity, uint32_t gen,
+                                  void* stream) {
+    if (!d_box || !d_claim || !d_activity) return RLE_E_INVAL;
+    const uint64_t tick_per_us = 100;   // wall_clock64: 100 MHz
+    hipLaunchKernelGGL(rle::svc_kernel, dim3(rle::kSvcGroups), dim3(rle::kWave * rle::kSvcWaves), 0,
+                       (hipStream_t)stream, (rle::SvcBox*)d_box, d_claim, d_activity, gen,
+                       tick_per_us * rle::kSvcIdleUs, tick_per_us * rle::kSvcLifeUs);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }

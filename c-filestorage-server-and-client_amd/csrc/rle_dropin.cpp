@@ -36,6 +36,7 @@
 #include "rleCompression.h"
 #include "rle_fileops.h"
 #include "rle_mi355x.h"
+#include "rle_service.h"
 
 // Measured-slower host-path variants (call coalescing, pipelined staging) are compiled only into the
 // test library (build/librle_mi355x_testhooks.so) and `make variant` builds, never into the product
@@ -144,6 +145,9 @@ size_t g_presize = 1u << 20;   // staging allocated with each thread context (pr
 // instead of hipStreamSynchronize (profiles/r4a_sync_probe.txt: 11.7 against 16.2 us per 4 KiB
 // launch).  RLE_MI355X_POLL=0: synchronize instead.
 bool g_poll = true;
+// Small calls through the resident service (rle_service.h) instead of a launch each:
+// RLE_MI355X_SERVICE=1 (off by default until measured).
+bool g_service = false;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 
 // Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
@@ -184,6 +188,8 @@ struct Ctx {
     uint8_t* h_cw = nullptr;                         // mapped launch words of combined launches (submit)
     uint8_t* d_cw = nullptr;
     uint32_t polled = 0;                             // polled launches since the last stream synchronize
+    int svc_slot = -2;                               // mailbox of the resident service (-1: none; -2: not yet asked)
+    uint32_t svc_seq = 0;                            // its latest request
 };
 // h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
 //   decode [in_off, in_len, out_off, out_len, out_cap, status], encode [in_off, in_len, out_off,
@@ -197,8 +203,10 @@ constexpr size_t kMetaDec = 0, kMetaEnc = 8, kMetaApp = 16, kMetaSlots = 24;
 pthread_mutex_t g_exit_lock = PTHREAD_MUTEX_INITIALIZER;
 bool g_exiting = false;
 void preinit_join();   // below
+void svc_stop();   // below
 void on_exit_handler() {
     preinit_join();   // (when called from the start-up thread's own exit: never; it makes no exit call)
+    svc_stop();
     pthread_mutex_lock(&g_exit_lock);
     g_exiting = true;
     pthread_mutex_unlock(&g_exit_lock);
@@ -238,6 +246,7 @@ void init_once() {
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
     if (const char* e = getenv("RLE_MI355X_POLL")) g_poll = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RLE_MI355X_SERVICE")) g_service = strcmp(e, "0") != 0;
 #if RLE_VARIANTS
     if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
 #endif
@@ -788,6 +797,122 @@ uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
     return v;
 }
 
+// ---------------------------------------------------------------- resident small-call service
+// (rle_service.h).  One service per process, on the device of the first context that asks (other
+// devices' contexts launch per call), on a stream of the greatest priority.  All state is constant-
+// initialised (POD); g_svc_m serialises set-up, launches and the stop.
+extern "C" int rle_service_launch(void* d_box, uint32_t* d_claim, unsigned long long* d_activity, uint32_t gen,
+                                  void* stream);
+pthread_mutex_t g_svc_m = PTHREAD_MUTEX_INITIALIZER;
+rle::SvcBox* g_svc_h = nullptr;        // mapped mailboxes (host address)
+rle::SvcBox* g_svc_d = nullptr;        // their device address
+uint32_t* g_svc_claim = nullptr;       // device: claimed sequence per slot
+unsigned long long* g_svc_act = nullptr;   // device: latest claim time
+hipStream_t g_svc_s = nullptr;
+int g_svc_dev = -1;
+int g_svc_state = 0;                   // 0 not set up, 1 ready, -1 unavailable
+std::atomic<uint32_t> g_svc_gen{0};    // generation of the latest launch (0: none yet)
+std::atomic<uint32_t> g_svc_next{0};   // next free slot
+
+bool svc_setup(int dev) {   // under g_svc_m
+    if (g_svc_state) return g_svc_state > 0;
+    g_svc_state = -1;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&g_svc_h), sizeof(rle::SvcBox), hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    memset(g_svc_h, 0, sizeof(rle::SvcBox));
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&g_svc_d), g_svc_h, 0) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&g_svc_claim), rle::kSvcSlots * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&g_svc_act), sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(g_svc_claim, 0, rle::kSvcSlots * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(g_svc_act, 0, sizeof(unsigned long long)) != hipSuccess ||
+        hipStreamCreateWithPriority(&g_svc_s, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamSynchronize(nullptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    g_svc_dev = dev;
+    g_svc_state = 1;
+    return true;
+}
+// The slot of context c (-1: the service is off, unavailable, full or on another device).
+int svc_slot(Ctx* c) {
+    if (c->svc_slot != -2) return c->svc_slot;
+    c->svc_slot = -1;
+    if (!g_service) return -1;
+    pthread_mutex_lock(&g_svc_m);
+    const bool ok = svc_setup(c->dev) && g_svc_dev == c->dev;
+    pthread_mutex_unlock(&g_svc_m);
+    if (!ok) return -1;
+    const uint32_t s = g_svc_next.fetch_add(1);
+    if (s >= rle::kSvcSlots) return -1;
+    c->svc_slot = (int)s;
+    c->svc_seq = __atomic_load_n(&g_svc_h->ack[s], __ATOMIC_ACQUIRE);   // (0: slots are never reused)
+    return c->svc_slot;
+}
+bool svc_all_gone(uint32_t gen) {
+    for (uint32_t g = 0; g < rle::kSvcGroups; ++g)
+        if (__atomic_load_n(&g_svc_h->gone[g], __ATOMIC_ACQUIRE) != gen) return false;
+    return true;
+}
+// A running service for the request just posted: launch one when there is none, or when every
+// workgroup of the latest has ended (its kernel is then complete: wait for it before the next).
+void svc_ensure() {
+    const uint32_t gen = g_svc_gen.load(std::memory_order_acquire);
+    if (gen && !svc_all_gone(gen)) return;
+    pthread_mutex_lock(&g_svc_m);
+    const uint32_t cur = g_svc_gen.load(std::memory_order_relaxed);
+    if (!cur || svc_all_gone(cur)) {
+        if (cur) check(hipStreamSynchronize(g_svc_s), "hipStreamSynchronize(service)");
+        __atomic_store_n(&g_svc_h->stop, 0u, __ATOMIC_RELEASE);
+        if (rle_service_launch(g_svc_d, g_svc_claim, g_svc_act, cur + 1u, g_svc_s) != RLE_OK)
+            die("service launch", hipGetLastError());
+        g_svc_gen.store(cur + 1u, std::memory_order_release);
+    }
+    pthread_mutex_unlock(&g_svc_m);
+}
+// At exit (on_exit_handler, before the runtime's teardown): end the service and wait for it.
+void svc_stop() {
+    pthread_mutex_lock(&g_svc_m);
+    if (g_svc_state > 0 && g_svc_gen.load()) {
+        __atomic_store_n(&g_svc_h->stop, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(g_svc_s);
+    }
+    pthread_mutex_unlock(&g_svc_m);
+}
+// One request of context c (slot >= 0) on its mapped buffer: returns the status, *res_len the
+// encoded size.  The wait polls ack[slot]; every 4096 polls it checks the service is still there.
+uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64_t cap, uint64_t* res_len) {
+    const int slot = c->svc_slot;
+    rle::SvcDesc* d = &g_svc_h->desc[slot];
+    d->src = reinterpret_cast<uint64_t>(c->d_zc + kZcIn);
+    d->dst = reinterpret_cast<uint64_t>(c->d_zc + kZcOut);
+    d->in_len = in_len;
+    d->out_len = out_len;
+    d->cap = cap;
+    d->op = op;
+    d->flags = 1u;   // write-through stores (the output leaves the L2 at once)
+    d->res_len = 0;
+    d->res_status = 0xFFFFFFFFu;
+    const uint32_t seq = ++c->svc_seq;
+    __atomic_store_n(&g_svc_h->req[slot], seq, __ATOMIC_RELEASE);
+    svc_ensure();
+    const uint64_t t0 = now_ns();
+    for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(&g_svc_h->ack[slot], __ATOMIC_ACQUIRE) == seq) break;
+        if ((i & 4095u) == 0u) {
+            svc_ensure();
+            if (now_ns() - t0 > 10000000000ull) die("service request (10 s)", hipErrorUnknown);
+        }
+        __builtin_ia32_pause();
+    }
+    if (res_len) *res_len = __atomic_load_n(&d->res_len, __ATOMIC_ACQUIRE);
+    return __atomic_load_n(&d->res_status, __ATOMIC_ACQUIRE);
+}
+
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, U);
@@ -800,7 +925,11 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
         C = r.result;
     } else
 #endif
-    {
+    if (svc_slot(c) >= 0) {
+        uint64_t Cs = 0;
+        check_encode_status(svc_call(c, rle::kSvcEncode, U, 0, 0, &Cs));
+        C = Cs;
+    } else {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = kPending;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
@@ -831,7 +960,9 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
         st = (uint32_t)r.result;
     } else
 #endif
-    {
+    if (svc_slot(c) >= 0) {
+        st = svc_call(c, rle::kSvcDecode, C, U, total, nullptr);
+    } else {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = kPending;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);

@@ -190,13 +190,57 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("poll", ["1", "0"])
-def test_polled_small_calls_bit_exact(poll):
+@pytest.mark.parametrize("poll,service", [("1", "0"), ("0", "0"), ("1", "1")])
+def test_polled_small_calls_bit_exact(poll, service):
     """The zero-copy small calls' completion: polling the status word the kernel stores behind a
-    system-scope release (RLE_MI355X_POLL=1, the default) or hipStreamSynchronize (=0).  600
+    system-scope release (RLE_MI355X_POLL=1, the default) or hipStreamSynchronize (=0), or the
+    resident service (RLE_MI355X_SERVICE=1: no launch per call, csrc/rle_service.h).  600
     consecutive calls of 0-16 KiB (cooperative and one-wave kernels), decodes with an extra region,
     serial-path streams, then 8 threads x 150 round trips, all against the oracle."""
-    env = dict(os.environ, RLE_MI355X_POLL=poll)
+    env = dict(os.environ, RLE_MI355X_POLL=poll, RLE_MI355X_SERVICE=service)
     r = subprocess.run([sys.executable, "-c", _POLL_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
+                        os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+
+
+_SERVICE_CODE = r"""
+import sys, threading, time
+sys.path[:0] = sys.argv[1:3]
+import rle_mi355x as R, rle_oracle as O
+errors = []
+# calls spaced past the service's idle time (1 ms): every call finds it gone and relaunches it
+for k in range(20):
+    x = O.gen(k % 5, 500 + k, 1000 + 700 * k)
+    y = O.encode(x)
+    if R.compress(x) != y or R.decompress(y, len(x)) != x:
+        errors.append(("gap", k))
+    time.sleep(0.003)
+# more threads than mailboxes (64): the contexts past them launch per call, side by side
+def work(t):
+    try:
+        for k in range(6):
+            U = 1 + (k * 3001 + t * 17) % 20000
+            x = O.gen((k + t) % 5, 70000 + 100 * t + k, U)
+            y = O.encode(x)
+            if R.compress(x) != y or R.decompress(y, U, 5) != x + bytes(5):
+                errors.append(("thread", t, k))
+    except Exception as e:
+        errors.append(repr(e))
+th = [threading.Thread(target=work, args=(t,)) for t in range(72)]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+assert not errors, errors[:5]
+print("ok")
+"""
+
+
+def test_service_relaunch_and_overflow_bit_exact():
+    """The resident service (RLE_MI355X_SERVICE=1) across its own idle exits (calls 3 ms apart: a
+    relaunch each) and with 72 threads, more contexts than it has mailboxes (the rest launch per
+    call), every stream against the oracle; the process then exits with the service stopped."""
+    env = dict(os.environ, RLE_MI355X_SERVICE="1")
+    r = subprocess.run([sys.executable, "-c", _SERVICE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
