@@ -40,10 +40,16 @@ def summarize(path):
 
 def main():
     exe = os.path.join(E.BIN, "server_gpu")
-    for name in ("battery1", "battery2", "battery3"):
+    for variant, extra in (("default", {}), ("service", {"RLE_MI355X_SERVICE": "1"})):
+        for name in ("battery1", "battery2", "battery3"):
+            run(exe, variant, extra, name)
+
+
+def run(exe, variant, extra, name):
+    if True:
         with tempfile.TemporaryDirectory() as tmp:
             tr = os.path.join(tmp, "trace.txt")
-            env = {"RLE_MI355X_TRACE": tr}
+            env = dict(extra, RLE_MI355X_TRACE=tr)
             if name == "battery1":
                 r = E.battery1(exe, os.path.join(tmp, "b"), env, EC.SETTLE)
                 E._check_battery1(r)
@@ -55,7 +61,7 @@ def main():
             else:
                 cold, hot = EC.battery3(exe, os.path.join(tmp, "b"), env)
                 wall = [cold, hot]
-            out = {"battery": name, "wall_s": wall}
+            out = {"variant": variant, "battery": name, "wall_s": wall}
             out.update(summarize(tr) if os.path.exists(tr) else {"trace": "missing"})
             print(json.dumps(out), flush=True)
 
