@@ -46,24 +46,23 @@ def main():
 
 
 def run(exe, variant, extra, name):
-    if True:
-        with tempfile.TemporaryDirectory() as tmp:
-            tr = os.path.join(tmp, "trace.txt")
-            env = dict(extra, RLE_MI355X_TRACE=tr)
-            if name == "battery1":
-                r = E.battery1(exe, os.path.join(tmp, "b"), env, EC.SETTLE)
-                E._check_battery1(r)
-                wall = r[3]
-            elif name == "battery2":
-                r = E.battery2(exe, os.path.join(tmp, "b"), env, EC.SETTLE)
-                E._check_battery2(r)
-                wall = r[3]
-            else:
-                cold, hot = EC.battery3(exe, os.path.join(tmp, "b"), env)
-                wall = [cold, hot]
-            out = {"variant": variant, "battery": name, "wall_s": wall}
-            out.update(summarize(tr) if os.path.exists(tr) else {"trace": "missing"})
-            print(json.dumps(out), flush=True)
+    with tempfile.TemporaryDirectory() as tmp:
+        tr = os.path.join(tmp, "trace.txt")
+        env = dict(extra, RLE_MI355X_TRACE=tr)
+        if name == "battery1":
+            r = E.battery1(exe, os.path.join(tmp, "b"), env, EC.SETTLE)
+            E._check_battery1(r)
+            wall = r[3]
+        elif name == "battery2":
+            r = E.battery2(exe, os.path.join(tmp, "b"), env, EC.SETTLE)
+            E._check_battery2(r)
+            wall = r[3]
+        else:
+            cold, hot = EC.battery3(exe, os.path.join(tmp, "b"), env)
+            wall = [cold, hot]
+        out = {"variant": variant, "battery": name, "wall_s": wall}
+        out.update(summarize(tr) if os.path.exists(tr) else {"trace": "missing"})
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
