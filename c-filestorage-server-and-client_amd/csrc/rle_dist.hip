@@ -282,7 +282,15 @@ extern "C" int rle_dist_gather_offsets_async(const int64_t* d_sizes, uint32_t n,
                                              void* comm_stream, int slot) {
     if (!g_comm) return RLE_E_INVAL;
     if (!d_sizes || !d_gathered || !d_offsets || (slot != 0 && slot != 1)) return RLE_E_INVAL;
-    if (slot == g_last_slot) return RLE_E_INVAL;
+    // a slot repeated while its previous exchange may still read sizes[slot] (the codec stream would
+    // wait only on the other slot's): refused; once that exchange has completed, a repeat is safe
+    if (slot == g_last_slot && g_done_rec[slot]) {
+        const hipError_t q = hipEventQuery(g_ev_done[slot]);
+        if (q != hipSuccess) {
+            (void)hipGetLastError();   // (hipErrorNotReady is not an error to report later)
+            return RLE_E_INVAL;
+        }
+    }
     for (int k = 0; k < 2; ++k) {
         if (!g_ev_enc[k] && hipEventCreateWithFlags(&g_ev_enc[k], hipEventDisableTiming) != hipSuccess) return RLE_E_HIP;
         if (!g_ev_done[k] && hipEventCreateWithFlags(&g_ev_done[k], hipEventDisableTiming) != hipSuccess) return RLE_E_HIP;

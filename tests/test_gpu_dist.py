@@ -131,7 +131,9 @@ def test_exchange_async_alternating_slots():
 
 
 def test_exchange_async_repeated_slot_refused():
-    """A repeated slot would make the codec stream wait on the stale other slot: refused."""
+    """A slot repeated while its previous exchange is still queued would let the codec stream wait
+    on the stale other slot: refused.  Once that exchange has completed (a warm-up
+    before the timed loop, bench.py), the repeat is accepted."""
     uid = R.dist_unique_id()
     R.dist_init(uid, 0, 1)
     try:
@@ -140,10 +142,17 @@ def test_exchange_async_repeated_slot_refused():
         sizes = torch.ones(n, dtype=torch.int64, device=DEV)
         g = torch.empty(n, dtype=torch.int64, device=DEV)
         o = torch.empty(n, dtype=torch.int64, device=DEV)
+        big = torch.empty(1 << 30, dtype=torch.uint8, device=DEV)
+        with torch.cuda.stream(comm):   # keeps the first exchange queued for a few ms
+            for _ in range(8):
+                big.fill_(1)
         R.dist_gather_offsets_async(sizes, g, o, codec, comm, 0)
         with pytest.raises(R.RLEError):
             R.dist_gather_offsets_async(sizes, g, o, codec, comm, 0)
         R.dist_gather_offsets_async(sizes, g, o, codec, comm, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(o, torch.arange(n, dtype=torch.int64, device=DEV))
+        R.dist_gather_offsets_async(sizes, g, o, codec, comm, 1)   # slot 1 again: its exchange is done
         torch.cuda.synchronize()
         assert torch.equal(o, torch.arange(n, dtype=torch.int64, device=DEV))
     finally:
