@@ -762,17 +762,20 @@ void submit(Ctx* c, Req* r) {
 #endif  // RLE_VARIANTS
 
 // Launch flags and completion wait of a zero-copy call (g_poll): the status word in the mapped
-// buffer is preset to kPending and polled.  Past kPollNs of polling (a box under load, a kernel
-// fault) the stream is synchronized, which also reports a failed launch; every kPollSyncEvery polled
-// calls it is synchronized anyway, so the runtime's record of completed launches stays short.
+// buffer is preset to kPending and polled, spinning for kSpinNs, then yielding the core between
+// reads.  Past kPollNs of polling (a box under load, a kernel fault) the stream is synchronized,
+// which also reports a failed launch; every kPollSyncEvery polled calls it is synchronized anyway,
+// so the runtime's record of completed launches stays short.
 constexpr uint32_t kPending = 0xFFFFFFFFu;
 constexpr uint64_t kPollNs = 2000000;
+constexpr uint64_t kSpinNs = 50000;   // then the poll yields the core between reads
 constexpr uint32_t kPollSyncEvery = 32;
 uint32_t zc_flags() { return g_poll ? RLE_LAUNCH_STATUS_FLAG : 0u; }
 uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
     const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(status_word);
     if (g_poll) {
         uint64_t t0 = 0;
+        bool yield = false;
         for (uint32_t i = 1;; ++i) {
             const uint32_t v = __atomic_load_n(st, __ATOMIC_ACQUIRE);
             if (v != kPending) {
@@ -782,12 +785,14 @@ uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
                 }
                 return v;
             }
-            if ((i & 255u) == 0u) {
+            if ((i & 63u) == 0u) {
                 const uint64_t t = now_ns();
                 if (!t0) t0 = t;
                 else if (t - t0 > kPollNs) break;
+                else yield = t - t0 > kSpinNs;
             }
-            __builtin_ia32_pause();
+            if (yield) sched_yield();   // a long call: leave the core to the server's other threads
+            else __builtin_ia32_pause();
         }
     }
     c->polled = 0;

@@ -9,6 +9,7 @@ usage: python tools/e2e_trace.py"""
 import collections
 import json
 import os
+import shutil
 import sys
 import tempfile
 
@@ -62,6 +63,10 @@ def run(exe, variant, extra, name):
             wall = [cold, hot]
         out = {"variant": variant, "battery": name, "wall_s": wall}
         out.update(summarize(tr) if os.path.exists(tr) else {"trace": "missing"})
+        keep = os.environ.get("E2E_TRACE_KEEP")   # a directory for the raw per-call traces
+        if keep and os.path.exists(tr):
+            os.makedirs(keep, exist_ok=True)
+            shutil.copyfile(tr, os.path.join(keep, f"{variant}_{name}.txt"))
         print(json.dumps(out), flush=True)
 
 
