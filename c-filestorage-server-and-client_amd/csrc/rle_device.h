@@ -1952,14 +1952,17 @@ __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u3
     RLE_STAMP(st.sp, 7);   // partial-chunk move, state
     return rounds;
 }
-template <bool kFast = false, u32 kChunks = kDecChunks>
+// kUni: the uniform-tile test first (dec_uniform_tile): the one-wave kernel's walk (r4b same-process
+// A/B: 64 KiB zero decode -1.9 %, 4 KiB zero -5 %, configs[1] -1 %), not the segmented write pass
+// (r4d: mixed batch +5 %, 1 MiB runs50 +3.8 % with it).
+template <bool kFast = false, u32 kChunks = kDecChunks, bool kUni = kFast>
 __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next, u32 pos, u32 C, u32 Co, u32 U,
                                         u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst, u32x4 rso,
                                         DecState& st, const DecK& kc, const u32x4* clut = nullptr) {
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
-    if (kFast && RLE_DEC_UNIFORM && !st.head && pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
+    if (kUni && RLE_DEC_UNIFORM && !st.head && pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
         u32 v;
         if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
             const u32 r = dec_fill_run(v, kUniformOut, lane, stage, rso, st);

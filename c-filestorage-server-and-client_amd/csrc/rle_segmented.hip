@@ -979,7 +979,7 @@ __device__ __forceinline__ void dec_seg_write(const uint8_t* src, uint8_t* dst, 
     const bool serial = walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         // the fast tile paths (round 3): past the segment's shared first chunk, and the literal
         // path only on tiles a later tile of this segment follows (dec_tile)
-        return dec_tile<RLE_SEG_FAST, kChunks>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc,
+        return dec_tile<RLE_SEG_FAST, kChunks, false>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc,
                                                clut);
     });
     dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
