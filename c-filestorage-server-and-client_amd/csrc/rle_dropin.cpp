@@ -148,6 +148,9 @@ bool g_poll = true;
 // Small calls through the resident service (rle_service.h) instead of a launch each:
 // RLE_MI355X_SERVICE=1 (off by default until measured).
 bool g_service = false;
+// Zero-copy calls from this many bytes (encode: U, decode: C) run the segmented kernels on the mapped
+// buffer instead of one wave walking it (RLE_MI355X_ZC_SEG=<bytes>; 0 = never).
+size_t g_zc_seg = 0;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 
 // Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
@@ -247,6 +250,7 @@ void init_once() {
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
     if (const char* e = getenv("RLE_MI355X_POLL")) g_poll = strcmp(e, "0") != 0;
     if (const char* e = getenv("RLE_MI355X_SERVICE")) g_service = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RLE_MI355X_ZC_SEG")) g_zc_seg = (size_t)strtoull(e, nullptr, 10);
 #if RLE_VARIANTS
     if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
 #endif
@@ -930,7 +934,18 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
         C = r.result;
     } else
 #endif
-    if (svc_slot(c) >= 0) {
+    if (g_zc_seg && U >= g_zc_seg) {   // several waves over the mapped buffer (segmented kernels)
+        uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
+        hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = 0;
+        uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+        grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, U));
+        if (rle_encode_batch_device_seg(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
+                                        reinterpret_cast<uint32_t*>(dw + 4), 1, U, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
+            die("encode launch", hipGetLastError());
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        check_encode_status((uint32_t)hw[4]);
+        C = hw[3];
+    } else if (svc_slot(c) >= 0) {
         uint64_t Cs = 0;
         check_encode_status(svc_call(c, rle::kSvcEncode, U, 0, 0, &Cs));
         C = Cs;
@@ -965,7 +980,17 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
         st = (uint32_t)r.result;
     } else
 #endif
-    if (svc_slot(c) >= 0) {
+    if (g_zc_seg && C >= g_zc_seg) {   // several waves over the mapped buffer (segmented kernels)
+        uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
+        hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
+        uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+        grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, C));
+        if (rle_decode_batch_device_seg(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
+                                        reinterpret_cast<uint32_t*>(dw + 5), 1, C, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
+            die("decode launch", hipGetLastError());
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        st = (uint32_t)hw[5];
+    } else if (svc_slot(c) >= 0) {
         st = svc_call(c, rle::kSvcDecode, C, U, total, nullptr);
     } else {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);

@@ -191,14 +191,15 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("poll,service", [("1", "0"), ("0", "0"), ("1", "1")])
-def test_polled_small_calls_bit_exact(poll, service):
+@pytest.mark.parametrize("poll,service,zcseg", [("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("1", "0", "8192")])
+def test_polled_small_calls_bit_exact(poll, service, zcseg):
     """The zero-copy small calls' completion: polling the status word the kernel stores behind a
     system-scope release (RLE_MI355X_POLL=1, the default) or hipStreamSynchronize (=0), or the
     resident service (RLE_MI355X_SERVICE=1: no launch per call, csrc/rle_service.h).  600
     consecutive calls of 0-16 KiB (cooperative and one-wave kernels), decodes with an extra region,
-    serial-path streams, then 8 threads x 150 round trips, all against the oracle."""
-    env = dict(os.environ, RLE_MI355X_POLL=poll, RLE_MI355X_SERVICE=service)
+    serial-path streams, then 8 threads x 150 round trips, all against the oracle.  zcseg: calls
+    from that many bytes run the segmented kernels on the mapped buffer (RLE_MI355X_ZC_SEG)."""
+    env = dict(os.environ, RLE_MI355X_POLL=poll, RLE_MI355X_SERVICE=service, RLE_MI355X_ZC_SEG=zcseg)
     r = subprocess.run([sys.executable, "-c", _POLL_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
