@@ -347,88 +347,62 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
 }
 
 // ================================================================ resident small-call service
-// (rle_service.h).  Wave 0 polls: lane s reads req[s] and claim[s]; the first pending slot this
-// workgroup claims (compare-and-swap of claim[s] from its last claimed sequence to the posted one)
-// is served by all kSvcWaves waves through the barrier-uniform codec bodies; every wave releases
-// its stores at system scope, and after a barrier thread 0 stores ack[s].  With nothing pending
-// anywhere for idle_ticks (the activity word: the latest claim of any workgroup), at life_ticks
-// after the launch, on the stop word, or after kSvcMaxPolls polls, the workgroup marks gone[g] and
-// ends.  The mailbox fields are read with system-scope atomic loads (vector loads that bypass the
-// caches; never the scalar cache).
-constexpr u32 kSvcNone = 0xFFFFFFFFu, kSvcExit = 0xFFFFFFFEu;
+// (rle_service.h): one workgroup per drop-in thread context.  Wave 0 polls the context's mailbox
+// line (lanes 0..15: one 64-byte read over PCIe with system-scope loads, then an acquire fence);
+// a new complete request (req != done, tail == req) is broadcast through LDS and served by all
+// kSvcWaves waves with the barrier-uniform codec bodies on the context's mapped buffer; every wave
+// releases its stores at system scope, and after a barrier thread 0 stores the result words and the
+// acknowledgement.  kSvcIdleUs after the last request, kSvcLifeUs after the launch, on the stop
+// word, or after kSvcMaxPolls polls, thread 0 marks `gone` with the launch's generation and the
+// workgroup ends.  Mailbox words are read only with vector loads (never the scalar cache).
 constexpr u32 kSvcUmax = 16384;
 constexpr u32 kSvcMaxPolls = 1u << 24;
-__device__ __forceinline__ u32 svc_ld(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t svc_ld64(const uint64_t* p) {
-    const uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return ((uint64_t)uniform((u32)(v >> 32)) << 32) | uniform((u32)v);
-}
-__global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcBox* box, uint32_t* __restrict__ claim,
-                                                              unsigned long long* __restrict__ activity, uint32_t gen,
-                                                              uint64_t idle_ticks, uint64_t life_ticks) {
-    __shared__ u32 sh[2];
+__global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcMail* mb, const uint8_t* src, uint8_t* dst,
+                                                              uint32_t gen, uint32_t done, uint64_t idle_ticks,
+                                                              uint64_t life_ticks) {
+    __shared__ u32 sh[8];   // 0: action (0 none, 1 serve, 2 exit); 1..7: words 1..7 of the line (7: tail = req)
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = coop_wave();
     const uint64_t t0 = wall_clock64();
+    uint64_t last = t0;
+    const uint32_t* line = reinterpret_cast<const uint32_t*>(&mb->r);
     for (u32 polls = 0;; ++polls) {
         if (wid == 0u) {
-            const u32 r = svc_ld(&box->req[lane]);
-            const u32 c = __hip_atomic_load(&claim[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t pend = __builtin_amdgcn_ballot_w64(r != c);
-            u32 slot = kSvcNone, seq = 0u;
-            while (pend) {   // another workgroup may claim a slot first
-                const u32 sl = (u32)__builtin_ctzll(pend);
-                pend &= pend - 1ull;
-                const u32 want = readlane(c, sl), got = readlane(r, sl);
-                u32 old = 0u;
-                if (lane == 0u) old = atomicCAS(&claim[sl], want, got);
-                if (readlane(old, 0) == want) {
-                    slot = sl;
-                    seq = got;
-                    break;
-                }
-            }
+            const u32 w = lane < 16u ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            const u32 req = readlane(w, 0), tail = readlane(w, 7), stop = readlane(w, 6);
             const uint64_t now = wall_clock64();
-            if (slot != kSvcNone) {
-                if (lane == 0u) atomicMax(activity, (unsigned long long)now);
-            } else {
-                const uint64_t act = __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t since = now - (act > t0 ? act : t0);
-                if (svc_ld(&box->stop) || since > idle_ticks || now - t0 > life_ticks || polls > kSvcMaxPolls)
-                    slot = kSvcExit;
+            u32 act = 0u;
+            if (req != done && tail == req) {
+                act = 1u;
+                last = now;
+            } else if (stop || now - last > idle_ticks || now - t0 > life_ticks || polls > kSvcMaxPolls) {
+                act = 2u;
             }
-            if (lane == 0u) {
-                sh[0] = slot;
-                sh[1] = seq;
-            }
+            if (lane < 8u) sh[lane] = lane == 0u ? act : w;
+            if (act == 1u) done = req;
         }
         __syncthreads();
-        const u32 slot = uniform(sh[0]), seq = uniform(sh[1]);
-        __syncthreads();   // (wave 0 rewrites sh at the next poll)
-        if (slot == kSvcExit) {
-            if (threadIdx.x == 0) __hip_atomic_store(&box->gone[blockIdx.x], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const u32 act = uniform(sh[0]);
+        if (act == 2u) {
+            if (threadIdx.x == 0) __hip_atomic_store(&mb->a.gone, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        if (slot == kSvcNone) {
-            __builtin_amdgcn_s_sleep(4);
-            continue;
-        }
-        SvcDesc* d = &box->desc[slot];
-        const u32 op = uniform(svc_ld(&d->op)), wt = uniform(svc_ld(&d->flags)) & kLaunchWt;
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(svc_ld64(&d->src));
-        uint8_t* dst = reinterpret_cast<uint8_t*>(svc_ld64(&d->dst));
-        const uint64_t in_len = svc_ld64(&d->in_len);
-        if (op == kSvcEncode) {
-            enc_coop_body<kSvcWaves, true>(src, dst, in_len, &d->res_len, &d->res_status, 0u, wt);
+        if (act == 1u) {
+            const u32 seq = uniform(sh[7]), op = uniform(sh[1]), in_len = uniform(sh[2]);
+            const u32 out_len = uniform(sh[3]), cap = uniform(sh[4]), wt = uniform(sh[5]) & kLaunchWt;
+            if (op == kSvcEncode) {
+                enc_coop_body<kSvcWaves, true>(src, dst, in_len, &mb->a.res_len, &mb->a.status, 0u, wt);
+            } else {
+                dec_coop_body<kSvcWaves, kSvcUmax, true>(src, dst, in_len, out_len, cap, &mb->a.status, 0u, wt);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's output, system scope
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(&mb->a.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
-            const uint64_t out_len = svc_ld64(&d->out_len), cap = svc_ld64(&d->cap);
-            dec_coop_body<kSvcWaves, kSvcUmax, true>(src, dst, in_len, out_len, cap, &d->res_status, 0u, wt);
+            __syncthreads();   // (wave 0 rewrites sh at the next poll)
+            __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's output, system scope
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(&box->ack[slot], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -553,14 +527,15 @@ extern "C" int rle_mi355x_set_coop_mode(int mode) {
     return RLE_OK;
 }
 
-// The resident small-call service (rle_service.h; launched by the drop-in, csrc/rle_dropin.cpp
-// svc_ensure): kSvcGroups workgroups of kSvcWaves waves on the caller's stream.
-extern "C" int rle_service_launch(void* d_box, uint32_t* d_claim, unsigned long long* d_activity, uint32_t gen,
+// The resident small-call service of one drop-in thread context (rle_service.h; launched by
+// csrc/rle_dropin.cpp svc_ensure): one workgroup of kSvcWaves waves on the given stream, serving
+// requests on the context's mapped buffer (d_src: input, d_dst: output) from sequence `done` on.
+extern "C" int rle_service_launch(void* d_mail, const void* d_src, void* d_dst, uint32_t gen, uint32_t done,
                                   void* stream) {
-    if (!d_box || !d_claim || !d_activity) return RLE_E_INVAL;
+    if (!d_mail || !d_src || !d_dst) return RLE_E_INVAL;
     const uint64_t tick_per_us = 100;   // wall_clock64: 100 MHz
-    hipLaunchKernelGGL(rle::svc_kernel, dim3(rle::kSvcGroups), dim3(rle::kWave * rle::kSvcWaves), 0,
-                       (hipStream_t)stream, (rle::SvcBox*)d_box, d_claim, d_activity, gen,
+    hipLaunchKernelGGL(rle::svc_kernel, dim3(1), dim3(rle::kWave * rle::kSvcWaves), 0, (hipStream_t)stream,
+                       (rle::SvcMail*)d_mail, (const uint8_t*)d_src, (uint8_t*)d_dst, gen, done,
                        tick_per_us * rle::kSvcIdleUs, tick_per_us * rle::kSvcLifeUs);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }

@@ -191,8 +191,12 @@ struct Ctx {
     uint8_t* h_cw = nullptr;                         // mapped launch words of combined launches (submit)
     uint8_t* d_cw = nullptr;
     uint32_t polled = 0;                             // polled launches since the last stream synchronize
-    int svc_slot = -2;                               // mailbox of the resident service (-1: none; -2: not yet asked)
-    uint32_t svc_seq = 0;                            // its latest request
+    int svc = -2;                                    // resident service (rle_service.h): 1 on, -1 off, -2 not yet asked
+    rle::SvcMail* svc_h = nullptr;                   // its mailbox (in the mapped zero-copy buffer) ...
+    rle::SvcMail* svc_d = nullptr;                   // ... and the mailbox's device address
+    hipStream_t svc_s = nullptr;                     // the service's stream
+    uint32_t svc_seq = 0;                            // latest request
+    uint32_t svc_gen = 0;                            // latest launch (0: none)
 };
 // h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
 //   decode [in_off, in_len, out_off, out_len, out_cap, status], encode [in_off, in_len, out_off,
@@ -207,6 +211,8 @@ pthread_mutex_t g_exit_lock = PTHREAD_MUTEX_INITIALIZER;
 bool g_exiting = false;
 void preinit_join();   // below
 void svc_stop();   // below
+void svc_end(Ctx* c);
+void svc_unregister(Ctx* c);
 void on_exit_handler() {
     preinit_join();   // (when called from the start-up thread's own exit: never; it makes no exit call)
     svc_stop();
@@ -224,6 +230,8 @@ void free_ctx(void* p) {
         return;
     }
     (void)hipSetDevice(c->dev);
+    svc_end(c);
+    svc_unregister(c);
     if (c->s) (void)hipStreamSynchronize(c->s);
     (void)hipHostFree(c->h_in);
     (void)hipHostFree(c->h_out);
@@ -807,119 +815,107 @@ uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
 }
 
 // ---------------------------------------------------------------- resident small-call service
-// (rle_service.h).  One service per process, on the device of the first context that asks (other
-// devices' contexts launch per call), on a stream of the greatest priority.  All state is constant-
-// initialised (POD); g_svc_m serialises set-up, launches and the stop.
-extern "C" int rle_service_launch(void* d_box, uint32_t* d_claim, unsigned long long* d_activity, uint32_t gen,
+// (rle_service.h): one resident workgroup per thread context, on the context's own service stream,
+// its mailbox in the context's mapped buffer.  g_svc_m guards the registry of contexts with a
+// service, which process exit stops (svc_stop).
+extern "C" int rle_service_launch(void* d_mail, const void* d_src, void* d_dst, uint32_t gen, uint32_t done,
                                   void* stream);
+constexpr size_t kZcMail = kZcWords + 2048;   // the mailbox's offset in the mapped buffer (64-byte aligned)
+constexpr int kSvcMax = 256;                  // contexts with a service at once (the rest launch per call)
 pthread_mutex_t g_svc_m = PTHREAD_MUTEX_INITIALIZER;
-rle::SvcBox* g_svc_h = nullptr;        // mapped mailboxes (host address)
-rle::SvcBox* g_svc_d = nullptr;        // their device address
-uint32_t* g_svc_claim = nullptr;       // device: claimed sequence per slot
-unsigned long long* g_svc_act = nullptr;   // device: latest claim time
-hipStream_t g_svc_s = nullptr;
-int g_svc_dev = -1;
-int g_svc_state = 0;                   // 0 not set up, 1 ready, -1 unavailable
-std::atomic<uint32_t> g_svc_gen{0};    // generation of the latest launch (0: none yet)
-std::atomic<uint32_t> g_svc_next{0};   // next free slot
+Ctx* g_svc_ctx[kSvcMax];
+int g_svc_n = 0;
 
-bool svc_setup(int dev) {   // under g_svc_m
-    if (g_svc_state) return g_svc_state > 0;
-    g_svc_state = -1;
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&g_svc_h), sizeof(rle::SvcBox), hipHostMallocMapped) != hipSuccess) {
+// Whether context c serves its small calls through its resident service (set up on first use).
+bool svc_on(Ctx* c) {
+    if (c->svc != -2) return c->svc > 0;
+    c->svc = -1;
+    if (!g_service) return false;
+    zc(c);
+    pthread_mutex_lock(&g_svc_m);
+    const bool room = g_svc_n < kSvcMax;
+    if (room) g_svc_ctx[g_svc_n++] = c;
+    pthread_mutex_unlock(&g_svc_m);
+    if (!room) return false;
+    if (hipStreamCreateWithFlags(&c->svc_s, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        c->svc_s = nullptr;
+        return false;   // (stays registered: svc_stop skips a context without a stream)
     }
-    memset(g_svc_h, 0, sizeof(rle::SvcBox));
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&g_svc_d), g_svc_h, 0) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&g_svc_claim), rle::kSvcSlots * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&g_svc_act), sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(g_svc_claim, 0, rle::kSvcSlots * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(g_svc_act, 0, sizeof(unsigned long long)) != hipSuccess ||
-        hipStreamCreateWithPriority(&g_svc_s, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipStreamSynchronize(nullptr) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    g_svc_dev = dev;
-    g_svc_state = 1;
+    c->svc_h = reinterpret_cast<rle::SvcMail*>(c->h_zc + kZcMail);
+    c->svc_d = reinterpret_cast<rle::SvcMail*>(c->d_zc + kZcMail);
+    memset(c->svc_h, 0, sizeof(rle::SvcMail));
+    c->svc = 1;
     return true;
 }
-// The slot of context c (-1: the service is off, unavailable, full or on another device).
-int svc_slot(Ctx* c) {
-    if (c->svc_slot != -2) return c->svc_slot;
-    c->svc_slot = -1;
-    if (!g_service) return -1;
-    pthread_mutex_lock(&g_svc_m);
-    const bool ok = svc_setup(c->dev) && g_svc_dev == c->dev;
-    pthread_mutex_unlock(&g_svc_m);
-    if (!ok) return -1;
-    const uint32_t s = g_svc_next.fetch_add(1);
-    if (s >= rle::kSvcSlots) return -1;
-    c->svc_slot = (int)s;
-    c->svc_seq = __atomic_load_n(&g_svc_h->ack[s], __ATOMIC_ACQUIRE);   // (0: slots are never reused)
-    return c->svc_slot;
+// A running service for c's request just posted: launch one when there is none or the last has ended
+// (wait for that launch to complete first).
+void svc_ensure(Ctx* c) {
+    if (c->svc_gen && __atomic_load_n(&c->svc_h->a.gone, __ATOMIC_ACQUIRE) != c->svc_gen) return;
+    if (c->svc_gen) check(hipStreamSynchronize(c->svc_s), "hipStreamSynchronize(service)");
+    const uint32_t done = __atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE);
+    if (rle_service_launch(c->svc_d, c->d_zc + kZcIn, c->d_zc + kZcOut, c->svc_gen + 1u, done, c->svc_s) != RLE_OK)
+        die("service launch", hipGetLastError());
+    ++c->svc_gen;
 }
-bool svc_all_gone(uint32_t gen) {
-    for (uint32_t g = 0; g < rle::kSvcGroups; ++g)
-        if (__atomic_load_n(&g_svc_h->gone[g], __ATOMIC_ACQUIRE) != gen) return false;
-    return true;
-}
-// A running service for the request just posted: launch one when there is none, or when every
-// workgroup of the latest has ended (its kernel is then complete: wait for it before the next).
-void svc_ensure() {
-    const uint32_t gen = g_svc_gen.load(std::memory_order_acquire);
-    if (gen && !svc_all_gone(gen)) return;
-    pthread_mutex_lock(&g_svc_m);
-    const uint32_t cur = g_svc_gen.load(std::memory_order_relaxed);
-    if (!cur || svc_all_gone(cur)) {
-        if (cur) check(hipStreamSynchronize(g_svc_s), "hipStreamSynchronize(service)");
-        __atomic_store_n(&g_svc_h->stop, 0u, __ATOMIC_RELEASE);
-        if (rle_service_launch(g_svc_d, g_svc_claim, g_svc_act, cur + 1u, g_svc_s) != RLE_OK)
-            die("service launch", hipGetLastError());
-        g_svc_gen.store(cur + 1u, std::memory_order_release);
+// End c's service and wait for it (thread exit, process exit).
+void svc_end(Ctx* c) {
+    if (c->svc <= 0 || !c->svc_s) return;
+    if (c->svc_gen) {
+        __atomic_store_n(&c->svc_h->r.stop, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(c->svc_s);
     }
+    (void)hipStreamDestroy(c->svc_s);
+    c->svc_s = nullptr;
+    c->svc = -1;
+}
+void svc_unregister(Ctx* c) {
+    pthread_mutex_lock(&g_svc_m);
+    for (int i = 0; i < g_svc_n; ++i)
+        if (g_svc_ctx[i] == c) {
+            g_svc_ctx[i] = g_svc_ctx[--g_svc_n];
+            break;
+        }
     pthread_mutex_unlock(&g_svc_m);
 }
-// At exit (on_exit_handler, before the runtime's teardown): end the service and wait for it.
+// At exit (on_exit_handler, before the runtime's teardown): every service ends.
 void svc_stop() {
     pthread_mutex_lock(&g_svc_m);
-    if (g_svc_state > 0 && g_svc_gen.load()) {
-        __atomic_store_n(&g_svc_h->stop, 1u, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(g_svc_s);
-    }
+    for (int i = 0; i < g_svc_n; ++i)
+        if (g_svc_ctx[i]->svc > 0 && g_svc_ctx[i]->svc_gen) __atomic_store_n(&g_svc_ctx[i]->svc_h->r.stop, 1u, __ATOMIC_RELEASE);
+    for (int i = 0; i < g_svc_n; ++i)
+        if (g_svc_ctx[i]->svc > 0 && g_svc_ctx[i]->svc_gen) (void)hipStreamSynchronize(g_svc_ctx[i]->svc_s);
     pthread_mutex_unlock(&g_svc_m);
 }
-// One request of context c (slot >= 0) on its mapped buffer: returns the status, *res_len the
-// encoded size.  The wait polls ack[slot]; every 4096 polls it checks the service is still there.
+// One request on c's mapped buffer: returns the status, *res_len the encoded size.  The line is
+// written with the sequence number last (tail, then req); the wait polls ack, checking every 256
+// polls that the service has not ended before taking the request.
 uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64_t cap, uint64_t* res_len) {
-    const int slot = c->svc_slot;
-    rle::SvcDesc* d = &g_svc_h->desc[slot];
-    d->src = reinterpret_cast<uint64_t>(c->d_zc + kZcIn);
-    d->dst = reinterpret_cast<uint64_t>(c->d_zc + kZcOut);
-    d->in_len = in_len;
-    d->out_len = out_len;
-    d->cap = cap;
-    d->op = op;
-    d->flags = 1u;   // write-through stores (the output leaves the L2 at once)
-    d->res_len = 0;
-    d->res_status = 0xFFFFFFFFu;
+    rle::SvcReq* r = &c->svc_h->r;
+    r->op = op;
+    r->in_len = (uint32_t)in_len;
+    r->out_len = (uint32_t)out_len;
+    r->cap = (uint32_t)cap;
+    r->flags = 1u;   // write-through stores (the output leaves the L2 at once)
     const uint32_t seq = ++c->svc_seq;
-    __atomic_store_n(&g_svc_h->req[slot], seq, __ATOMIC_RELEASE);
-    svc_ensure();
+    __atomic_store_n(&r->tail, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&r->req, seq, __ATOMIC_RELEASE);
+    svc_ensure(c);
     const uint64_t t0 = now_ns();
+    bool yield = false;
     for (uint32_t i = 1;; ++i) {
-        if (__atomic_load_n(&g_svc_h->ack[slot], __ATOMIC_ACQUIRE) == seq) break;
-        if ((i & 4095u) == 0u) {
-            svc_ensure();
-            if (now_ns() - t0 > 10000000000ull) die("service request (10 s)", hipErrorUnknown);
+        if (__atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE) == seq) break;
+        if ((i & 255u) == 0u) {
+            svc_ensure(c);
+            const uint64_t t = now_ns() - t0;
+            if (t > 10000000000ull) die("service request (10 s)", hipErrorUnknown);
+            yield = t > kSpinNs;
         }
-        __builtin_ia32_pause();
+        if (yield) sched_yield();
+        else __builtin_ia32_pause();
     }
-    if (res_len) *res_len = __atomic_load_n(&d->res_len, __ATOMIC_ACQUIRE);
-    return __atomic_load_n(&d->res_status, __ATOMIC_ACQUIRE);
+    if (res_len) *res_len = __atomic_load_n(&c->svc_h->a.res_len, __ATOMIC_ACQUIRE);
+    return __atomic_load_n(&c->svc_h->a.status, __ATOMIC_ACQUIRE);
 }
 
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
@@ -945,7 +941,7 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
         check_encode_status((uint32_t)hw[4]);
         C = hw[3];
-    } else if (svc_slot(c) >= 0) {
+    } else if (svc_on(c)) {
         uint64_t Cs = 0;
         check_encode_status(svc_call(c, rle::kSvcEncode, U, 0, 0, &Cs));
         C = Cs;
@@ -990,7 +986,7 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
             die("decode launch", hipGetLastError());
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
         st = (uint32_t)hw[5];
-    } else if (svc_slot(c) >= 0) {
+    } else if (svc_on(c)) {
         st = svc_call(c, rle::kSvcDecode, C, U, total, nullptr);
     } else {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);

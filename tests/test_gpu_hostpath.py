@@ -217,7 +217,7 @@ for k in range(20):
     if R.compress(x) != y or R.decompress(y, len(x)) != x:
         errors.append(("gap", k))
     time.sleep(0.003)
-# more threads than mailboxes (64): the contexts past them launch per call, side by side
+# many threads at once: one resident service workgroup each
 def work(t):
     try:
         for k in range(6):
@@ -240,8 +240,8 @@ print("ok")
 
 def test_service_relaunch_and_overflow_bit_exact():
     """The resident service (RLE_MI355X_SERVICE=1) across its own idle exits (calls 3 ms apart: a
-    relaunch each) and with 72 threads, more contexts than it has mailboxes (the rest launch per
-    call), every stream against the oracle; the process then exits with the service stopped."""
+    relaunch each) and with 72 threads at once (72 resident workgroups, one per thread context),
+    every stream against the oracle; the process then exits with every service stopped."""
     env = dict(os.environ, RLE_MI355X_SERVICE="1")
     r = subprocess.run([sys.executable, "-c", _SERVICE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
