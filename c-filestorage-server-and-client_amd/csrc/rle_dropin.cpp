@@ -152,6 +152,7 @@ bool g_service = false;
 // buffer instead of one wave walking it (RLE_MI355X_ZC_SEG=<bytes>; 0 = never).
 size_t g_zc_seg = 0;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
+constexpr size_t kZcMaxIn = kZcWords, kZcMaxOut = kZcBytes - kZcOut;   // one zero-copy call's bytes
 
 // Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
 // staged input (and output) bytes, and a file larger than that is copied straight from / to the
@@ -1147,7 +1148,8 @@ bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* a
 
 static char* compress_impl(char* data, size_t U, size_t* compressedSize) {
     Ctx* c = ctx();
-    if (U < kSegEncodeBytes) {   // one wave walks it: the single-copy path
+    // one wave walks it, or (g_zc_seg) the segmented kernels on the mapped buffer: the single-copy path
+    if (U < kSegEncodeBytes || (g_zc_seg && g_zerocopy && U <= kZcMaxIn)) {
         const uint64_t t0 = now_ns();
         char* r = compress_small(c, data, U, compressedSize);
         g_stats.calls_compress++;
@@ -1210,7 +1212,9 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
 static void decompress_impl(char* data, size_t C, size_t U, size_t E, char* r) {
     const size_t total = U + E;
     Ctx* c = ctx();
-    if (C < kSegDecodeBytes && total <= kOneTripBytes) {   // one wave walks it: the single-copy path
+    // one wave walks it, or (g_zc_seg) the segmented kernels on the mapped buffer: the single-copy path
+    if ((C < kSegDecodeBytes && total <= kOneTripBytes) ||
+        (g_zc_seg && g_zerocopy && C <= kZcMaxIn && total <= kZcMaxOut)) {
         const uint64_t t0 = now_ns();
         decompress_small(c, data, C, U, E, r);
         g_stats.calls_decompress++;

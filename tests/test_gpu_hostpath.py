@@ -170,6 +170,18 @@ for k in range(600):
         if R.decompress(s, U, 64) != O.decode(s, U, U + 64)[0]:
             errors.append(("serial", k, U))
 
+# 32-64 KiB calls (the zero-copy segmented form's upper range with RLE_MI355X_ZC_SEG; the copying
+# large-call form otherwise), exactly 64 KiB, and decodes with a large extra region
+for k in range(40):
+    U = 65536 if k % 10 == 9 else 32768 + (k * 997) % 32768
+    x = O.gen(k % 5, 60000 + k, U)
+    y = O.encode(x)
+    if R.compress(x) != y:
+        errors.append(("enc-mid", k, U))
+    E = 50000 if k % 3 == 0 else 0
+    if R.decompress(y, U, E) != x + bytes(E):
+        errors.append(("dec-mid", k, U, E))
+
 def work(t):
     try:
         for k in range(150):
