@@ -198,6 +198,7 @@ struct Ctx {
     hipStream_t svc_s = nullptr;                     // the service's stream
     uint32_t svc_seq = 0;                            // latest request
     uint32_t svc_gen = 0;                            // latest launch (0: none)
+    bool full = false;                               // presized and warmed for large calls (preinit)
 };
 // h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
 //   decode [in_off, in_len, out_off, out_len, out_cap, status], encode [in_off, in_len, out_off,
@@ -283,9 +284,10 @@ inline size_t round16(size_t x) { return (x + 15u) & ~(size_t)15u; }
 
 void presize(Ctx* c);   // below
 void warm(Ctx* c);      // below
+void warm_small(Ctx* c);   // below
 
-// A context on device dev: its stream, launch words and (presize) staging.  Throws std::bad_alloc.
-Ctx* new_ctx(int dev) {
+// A context on device dev: its stream, launch words and (sized) staging.  Throws std::bad_alloc.
+Ctx* new_ctx(int dev, bool sized = true) {
     Ctx* c = new Ctx();
     c->dev = dev;
     check(hipSetDevice(c->dev), "hipSetDevice");
@@ -298,7 +300,8 @@ Ctx* new_ctx(int dev) {
         delete c;
         throw std::bad_alloc();
     }
-    presize(c);
+    if (sized) presize(c);
+    c->full = sized;
     return c;
 }
 
@@ -309,10 +312,13 @@ Ctx* new_ctx(int dev) {
 // engines (e2e battery 1: 89-167 ms against the reference's 5-7 ms; ns_stage_in 7.75 ms for 883 KB).
 // Now the library's constructor starts one background thread when it is loaded, before main() runs
 // in a server that links it: the thread initialises the runtime and builds RLE_MI355X_PREINIT
-// contexts (default 8; 0 = off, the round-3 behaviour), each warmed with one call of every transfer
-// form (zero-copy, pinned, pageable) and every kernel form, and puts them in a pool.  A worker's first
-// call takes a warm context from the pool (waiting for the thread if it is still building them), and
-// makes its own only when the pool is empty.  Process exit stops the thread between two steps and
+// contexts (default 8; 0 = off, the round-3 behaviour) in two phases: first each ready for small
+// calls (stream, launch words, zero-copy buffer, one small call each way) and put in a pool, then
+// those still in the pool sized and warmed with one call of every transfer form (pinned, pageable)
+// and kernel form (r4e trace: with one phase, 8 worker threads writing at once on a fresh server
+// waited 32, 17, 10, 10, 4, 4 and 4 ms in turn for their contexts, serialised by the store lock).
+// A worker's first call takes a context from the pool (waiting for the thread if it is still
+// building them), and makes its own only when the pool is empty.  Process exit stops the thread between two steps and
 // waits for it (preinit_exit, registered before the thread starts), so it never runs into the
 // runtime's teardown.
 // Everything the start-up thread touches is constant-initialised (POD, pthread static
@@ -333,16 +339,43 @@ void* preinit_main(void*) {
     if (const char* e = getenv("RLE_MI355X_PREINIT")) want = atoi(e);
     want = want < kPoolMax ? want : kPoolMax;
     pthread_once(&g_once, init_once);
+    // phase 1: every context ready for small calls (stream, launch words, zero-copy buffer, one
+    // small call each way), so that the worker threads' first calls wait as little as possible
     for (int i = 0; i < want && g_ndev > 0 && !g_pre_stop.load(); ++i) {
         const int dev = (g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev);
         Ctx* c = nullptr;
         try {
-            c = new_ctx(dev);
-            warm(c);
+            c = new_ctx(dev, false);
+            warm_small(c);
         } catch (const std::bad_alloc&) {
             if (c) free_ctx(c);
             break;
         }
+        pthread_mutex_lock(&g_pool_m);
+        g_pool[g_pool_n++] = c;
+        pthread_cond_broadcast(&g_pool_cv);
+        pthread_mutex_unlock(&g_pool_m);
+    }
+    // phase 2: the contexts still in the pool, one at a time, sized and warmed for large calls (a
+    // context a worker has taken meanwhile grows its staging on demand instead)
+    while (!g_pre_stop.load()) {
+        Ctx* c = nullptr;
+        pthread_mutex_lock(&g_pool_m);
+        for (int i = 0; i < g_pool_n; ++i)
+            if (!g_pool[i]->full) {
+                c = g_pool[i];
+                g_pool[i] = g_pool[--g_pool_n];
+                break;
+            }
+        pthread_mutex_unlock(&g_pool_m);
+        if (!c) break;
+        try {
+            check(hipSetDevice(c->dev), "hipSetDevice");
+            presize(c);
+            warm(c);
+        } catch (const std::bad_alloc&) {
+        }
+        c->full = true;   // (also after an allocation failure: not tried again)
         pthread_mutex_lock(&g_pool_m);
         g_pool[g_pool_n++] = c;
         pthread_cond_broadcast(&g_pool_cv);
@@ -1063,6 +1096,17 @@ void decompress_small(Ctx* c, const char* data, size_t C, size_t U, size_t E, ch
 // use: the zero-copy small calls (one-wave and cooperative kernels), a segmented encode + decode
 // through the pinned staging, and the runtime's pageable-memory copies of large calls (direct
 // staging), which set up the copy engines and the runtime's own staging buffers on first use.
+// One small call each way (phase 1 of the start-up): the zero-copy buffer and the stream's first
+// launches.
+void warm_small(Ctx* c) {
+    uint8_t buf[4096], back[4096];
+    for (size_t i = 0; i < sizeof(buf); ++i) buf[i] = (uint8_t)(((i * 2654435761u) >> 13) & 3u);
+    size_t C = 0;
+    char* r = compress_small(c, reinterpret_cast<const char*>(buf), sizeof(buf), &C);
+    if (!r) throw std::bad_alloc();
+    decompress_small(c, r, C, sizeof(buf), 0, reinterpret_cast<char*>(back));
+    free(r);
+}
 void warm(Ctx* c) {
     constexpr size_t kBig = kPipeMinBytes + (64u << 10), kMed = 64u << 10, kSmall = 4096;
     std::vector<uint8_t> buf(kBig), back(kBig);
