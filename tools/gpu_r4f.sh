@@ -27,4 +27,8 @@ for U in 8192 16384 24576 40000; do
     done
   done
 done
+E2E_TRACE_KEEP=$O/traces timeout -k 10 300 python -u $R/tools/e2e_trace.py > $O/e2e_trace.json 2> $O/e2e_trace.err
+rc=$?; echo "e2e_trace rc=$rc" >> $O/status; fatal $rc
+timeout -k 10 500 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
+rc=$?; echo "e2e_compare rc=$rc" >> $O/status; fatal $rc
 exit 0
