@@ -34,12 +34,13 @@ constexpr u32 kCoopMaxWaves = 8;
 
 __device__ __forceinline__ u32 coop_wave() { return uniform(threadIdx.x / kWave); }
 
-// Completion-flag launches (put_status): every wave that stored output releases its stores before
-// the barrier behind which thread 0 stores the status.  All waves still running reach it (the
-// waves without a tile ended before the first barrier).
+// Completion-flag launches (put_status): every wave waits for its stores' acknowledgements (they
+// are in the XCD's L2, or past it) before the barrier behind which thread 0 releases them all at
+// system scope (one L2 write-back, in put_status) and stores the status.  All waves still running
+// reach the barrier (the waves without a tile ended before the first one).
 __device__ __forceinline__ void coop_release(u32 flags) {
     if (flags & kLaunchFlag) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        vm_drain();
         __syncthreads();
     }
 }
@@ -348,10 +349,11 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
 
 // ================================================================ resident small-call service
 // (rle_service.h): one workgroup per drop-in thread context.  Wave 0 polls the context's mailbox
-// line (lanes 0..15: one 64-byte read over PCIe with system-scope loads, then an acquire fence);
+// line (lanes 0..15: one 64-byte read over PCIe with system-scope loads; an acquire fence once a
+// request is seen);
 // a new complete request (req != done, tail == req) is broadcast through LDS and served by all
 // kSvcWaves waves with the barrier-uniform codec bodies on the context's mapped buffer; every wave
-// releases its stores at system scope, and after a barrier thread 0 stores the result words and the
+// waits for its stores, and after a barrier thread 0 releases them at system scope and stores the
 // acknowledgement.  kSvcIdleUs after the last request, kSvcLifeUs after the launch, on the stop
 // word, or after kSvcMaxPolls polls, thread 0 marks `gone` with the launch's generation and the
 // workgroup ends.  Mailbox words are read only with vector loads (never the scalar cache).
@@ -369,11 +371,13 @@ __global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcMail* mb, cons
     for (u32 polls = 0;; ++polls) {
         if (wid == 0u) {
             const u32 w = lane < 16u ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             const u32 req = readlane(w, 0), tail = readlane(w, 7), stop = readlane(w, 6);
             const uint64_t now = wall_clock64();
             u32 act = 0u;
             if (req != done && tail == req) {
+                // acquire once per request, not per poll (a system-scope acquire invalidates the
+                // XCD's L2: per poll, 8 resident workgroups slowed every other's request, r4f)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 act = 1u;
                 last = now;
             } else if (stop || now - last > idle_ticks || now - t0 > life_ticks || polls > kSvcMaxPolls) {
@@ -396,9 +400,12 @@ __global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcMail* mb, cons
             } else {
                 dec_coop_body<kSvcWaves, kSvcUmax, true>(src, dst, in_len, out_len, cap, &mb->a.status, 0u, wt);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's output, system scope
+            vm_drain();   // this wave's stores acknowledged (in the L2 or past it) ...
             __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_store(&mb->a.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (threadIdx.x == 0) {   // ... then one system-scope release of them all and the acknowledgement
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                __hip_atomic_store(&mb->a.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         } else {
             __syncthreads();   // (wave 0 rewrites sh at the next poll)
             __builtin_amdgcn_s_sleep(2);

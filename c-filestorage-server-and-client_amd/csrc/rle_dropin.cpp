@@ -149,8 +149,11 @@ bool g_poll = true;
 // RLE_MI355X_SERVICE=1 (off by default until measured).
 bool g_service = false;
 // Zero-copy calls from this many bytes (encode: U, decode: C) run the segmented kernels on the mapped
-// buffer instead of one wave walking it (RLE_MI355X_ZC_SEG=<bytes>; 0 = never).
-size_t g_zc_seg = 0;
+// buffer instead of one wave walking it, and the zero-copy form then takes calls up to 64 KiB in
+// (RLE_MI355X_ZC_SEG=<bytes>; 0 = never).  profiles/r4f_callrate_zcseg.txt, µs per call on 1 / 8
+// threads: 40 KB 42.2 / 91.7 against 66.1 / 151.3 for one wave over the mapped buffer; 24 KiB
+// 41.2 / 91.1 against 34.8 / 64.2 (the five launches cost more than a short walk).
+size_t g_zc_seg = 32u << 10;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 constexpr size_t kZcMaxIn = kZcWords, kZcMaxOut = kZcBytes - kZcOut;   // one zero-copy call's bytes
 
@@ -330,6 +333,7 @@ pthread_cond_t g_pool_cv = PTHREAD_COND_INITIALIZER;
 Ctx* g_pool[kPoolMax];
 int g_pool_n = 0;                    // under g_pool_m
 bool g_pre_running = false;          // under g_pool_m
+bool g_pre_phase1 = false;           // under g_pool_m: phase 1 (contexts still being made) running
 std::atomic<bool> g_pre_stop{false};
 pthread_t g_pre_thread;
 std::atomic<bool> g_pre_started{false};
@@ -357,7 +361,12 @@ void* preinit_main(void*) {
         pthread_mutex_unlock(&g_pool_m);
     }
     // phase 2: the contexts still in the pool, one at a time, sized and warmed for large calls (a
-    // context a worker has taken meanwhile grows its staging on demand instead)
+    // context a worker has taken meanwhile grows its staging on demand instead).  A worker that
+    // finds the pool empty now makes its own context rather than wait for this one (r4f trace).
+    pthread_mutex_lock(&g_pool_m);
+    g_pre_phase1 = false;
+    pthread_cond_broadcast(&g_pool_cv);
+    pthread_mutex_unlock(&g_pool_m);
     while (!g_pre_stop.load()) {
         Ctx* c = nullptr;
         pthread_mutex_lock(&g_pool_m);
@@ -383,6 +392,7 @@ void* preinit_main(void*) {
     }
     pthread_mutex_lock(&g_pool_m);
     g_pre_running = false;
+    g_pre_phase1 = false;
     pthread_cond_broadcast(&g_pool_cv);
     pthread_mutex_unlock(&g_pool_m);
     return nullptr;
@@ -403,15 +413,15 @@ __attribute__((constructor)) void preinit_start() {
     if (e && atoi(e) <= 0) return;
     atexit(preinit_exit);
     pthread_mutex_lock(&g_pool_m);
-    g_pre_running = true;
+    g_pre_running = g_pre_phase1 = true;
     if (pthread_create(&g_pre_thread, nullptr, preinit_main, nullptr) == 0) g_pre_started.store(true);
-    else g_pre_running = false;
+    else g_pre_running = g_pre_phase1 = false;
     pthread_mutex_unlock(&g_pool_m);
 }
 // A warm context from the pool, or nullptr (none left and the thread has finished).
 Ctx* pool_take() {
     pthread_mutex_lock(&g_pool_m);
-    while (g_pool_n == 0 && g_pre_running) pthread_cond_wait(&g_pool_cv, &g_pool_m);
+    while (g_pool_n == 0 && g_pre_phase1) pthread_cond_wait(&g_pool_cv, &g_pool_m);
     Ctx* c = g_pool_n ? g_pool[--g_pool_n] : nullptr;
     pthread_mutex_unlock(&g_pool_m);
     return c;
@@ -431,7 +441,8 @@ Ctx* ctx() {
     const uint64_t t0 = g_trace ? now_ns() : 0;
     c = pool_take();
     if (c) check(hipSetDevice(c->dev), "hipSetDevice");
-    else c = new_ctx((g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev));
+    else c = new_ctx((g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev),
+                     !g_pre_started.load());   // (beside the start-up thread: unsized, for a short first call)
     pthread_setspecific(g_key, c);
     if (g_trace) t_ctx_ns = now_ns() - t0;
     return c;
