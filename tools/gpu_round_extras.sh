@@ -1,0 +1,23 @@
+#!/bin/bash
+# Second half of a GPU round (after tools/gpu_round.sh): the per-kind SQ counters of the codec
+# kernels (tools/gpu_sq_kinds.sh -> tools/sq_kinds_table.py), the drop-in's call rates and the
+# unchanged server side by side (tools/e2e_compare.py).   usage: bash tools/gpu_round_extras.sh TAG
+set -o pipefail
+TAG=${1:-round}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+hostname > $O/host_extras.txt
+fatal() { case $1 in 124|134|137|139) exit $1;; esac; }
+bash $R/tools/gpu_sq_kinds.sh ${TAG}_sq k64_zero k64_random k64_runs50 k64_runs90 cfg1
+rc=$?; echo "sq rc=$rc" >> $O/status_extras; fatal $rc
+for S in 0 1; do
+  for T in 1 8 16; do
+    echo "service=$S U=4096 threads=$T" >> $O/callrate.txt
+    RLE_MI355X_SERVICE=$S timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
+    rc=$?; echo "callrate service=$S $T rc=$rc" >> $O/status_extras; fatal $rc
+  done
+done
+timeout -k 10 500 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
+rc=$?; echo "e2e_compare rc=$rc" >> $O/status_extras; fatal $rc
+exit 0
