@@ -102,7 +102,9 @@ def test_concurrent_small_calls_coalesced_bit_exact():
     threads, each 40 round trips of its own 4 KiB - 40 KiB buffers through the drop-in, every stream
     against the oracle; the library counts every small call as combined."""
     # (no background start-up: its warm-up calls would be combined too, after the counters' reset)
-    env = dict(os.environ, RLE_MI355X_COALESCE="1", RLE_MI355X_LIB=VARIANTS_LIB, RLE_MI355X_PREINIT="0")
+    # (and the one-wave zero-copy range only: the count below is of calls under 48 / 32 KiB)
+    env = dict(os.environ, RLE_MI355X_COALESCE="1", RLE_MI355X_LIB=VARIANTS_LIB, RLE_MI355X_PREINIT="0",
+               RLE_MI355X_ZC_SEG="0")
     r = subprocess.run([sys.executable, "-c", _COALESCE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
