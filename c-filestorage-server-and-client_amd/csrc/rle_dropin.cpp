@@ -342,14 +342,21 @@ void* preinit_main(void*) {
     int want = 8;
     if (const char* e = getenv("RLE_MI355X_PREINIT")) want = atoi(e);
     want = want < kPoolMax ? want : kPoolMax;
-    pthread_once(&g_once, init_once);
+    {
+        TraceScope ts('I', 0, 0, 0);   // (trace record: the runtime's start-up)
+        pthread_once(&g_once, init_once);
+    }
     // phase 1: every context ready for small calls (stream, launch words, zero-copy buffer, one
     // small call each way), so that the worker threads' first calls wait as little as possible
     for (int i = 0; i < want && g_ndev > 0 && !g_pre_stop.load(); ++i) {
         const int dev = (g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev);
         Ctx* c = nullptr;
         try {
-            c = new_ctx(dev, false);
+            TraceScope ts('P', 1, (uint64_t)i, 0);   // (trace records: each context's phase-1 set-up ...)
+            {
+                TraceScope tn('N', 1, (uint64_t)i, 0);   // (... of which making the context)
+                c = new_ctx(dev, false);
+            }
             warm_small(c);
         } catch (const std::bad_alloc&) {
             if (c) free_ctx(c);
@@ -379,6 +386,7 @@ void* preinit_main(void*) {
         pthread_mutex_unlock(&g_pool_m);
         if (!c) break;
         try {
+            TraceScope ts('P', 2, 0, 0);   // (trace record: one context's phase-2 sizing and warm-up)
             check(hipSetDevice(c->dev), "hipSetDevice");
             presize(c);
             warm(c);

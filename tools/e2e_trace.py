@@ -18,7 +18,8 @@ sys.path[:0] = [os.path.join(REPO, "tests"), os.path.join(REPO, "tools")]
 import e2e_compare as EC  # noqa: E402
 import test_e2e_server as E  # noqa: E402
 
-OPS = {"c": "RLEcompress", "d": "RLEdecompress", "a": "RLEappend", "n": "RLEdecompressN"}
+OPS = {"c": "RLEcompress", "d": "RLEdecompress", "a": "RLEappend", "n": "RLEdecompressN",
+       "I": "start-up: runtime", "P": "start-up: context", "N": "start-up: new context"}
 
 
 def summarize(path):
@@ -31,10 +32,13 @@ def summarize(path):
     for r in recs:
         by[r["op"]][0] += 1
         by[r["op"]][1] += r["dt"]
+    start = [r for r in recs if r["op"].startswith("start-up")]
+    recs = [r for r in recs if not r["op"].startswith("start-up")]
     slow = sorted(recs, key=lambda r: -r["dt"])[:12]
     return {"calls": {k: {"n": v[0], "ms": round(v[1] / 1e6, 3)} for k, v in by.items()},
             "ctx_ms": round(sum(r["ctx"] for r in recs) / 1e6, 3),
             "threads": len({r["tid"] for r in recs}),
+            "start_up_ms": [(r["op"][10:], r["a"], r["b"], round(r["dt"] / 1e6, 2)) for r in sorted(start, key=lambda r: r["t0"])],
             "slowest": [{"op": r["op"], "sizes": [r["a"], r["b"], r["c"]], "us": round(r["dt"] / 1e3, 1),
                          "ctx_us": round(r["ctx"] / 1e3, 1)} for r in slow]}
 
