@@ -315,10 +315,10 @@ Ctx* new_ctx(int dev, bool sized = true) {
 // engines (e2e battery 1: 89-167 ms against the reference's 5-7 ms; ns_stage_in 7.75 ms for 883 KB).
 // Now the library's constructor starts one background thread when it is loaded, before main() runs
 // in a server that links it: the thread initialises the runtime and builds RLE_MI355X_PREINIT
-// contexts (default 8; 0 = off, the round-3 behaviour) in two phases: first each ready for small
-// calls (stream, launch words, zero-copy buffer, one small call each way) and put in a pool, then
-// those still in the pool sized and warmed with one call of every transfer form (pinned, pageable)
-// and kernel form (r4e trace: with one phase, 8 worker threads writing at once on a fresh server
+// contexts (default 8; 0 = off, the round-3 behaviour) in two phases: first one sized and warmed
+// with one call of every transfer form (pinned, pageable) and kernel form, and the others only
+// ready for small calls (stream, launch words, zero-copy buffer, one small call each way), each put
+// in the pool as soon as it is ready; then those still in the pool sized and warmed too (r4e trace: with one phase, 8 worker threads writing at once on a fresh server
 // waited 32, 17, 10, 10, 4, 4 and 4 ms in turn for their contexts, serialised by the store lock).
 // A worker's first call takes a context from the pool (waiting for the thread if it is still
 // building them), and makes its own only when the pool is empty.  Process exit stops the thread between two steps and
@@ -355,9 +355,14 @@ void* preinit_main(void*) {
             TraceScope ts('P', 1, (uint64_t)i, 0);   // (trace records: each context's phase-1 set-up ...)
             {
                 TraceScope tn('N', 1, (uint64_t)i, 0);   // (... of which making the context)
-                c = new_ctx(dev, false);
+                c = new_ctx(dev, i == 0);
             }
-            warm_small(c);
+            // the first context sized and warmed for every call form at once: the process-wide
+            // first uses (each kernel's first launch, the runtime's copy paths) are then done before
+            // a worker's first large call (r4 e2e: with every context light first, the first large
+            // calls spent 26.6 ms staging in against 0.07 ms)
+            if (i == 0) warm(c);
+            else warm_small(c);
         } catch (const std::bad_alloc&) {
             if (c) free_ctx(c);
             break;
@@ -430,6 +435,13 @@ __attribute__((constructor)) void preinit_start() {
 Ctx* pool_take() {
     pthread_mutex_lock(&g_pool_m);
     while (g_pool_n == 0 && g_pre_phase1) pthread_cond_wait(&g_pool_cv, &g_pool_m);
+    for (int i = 0; i + 1 < g_pool_n; ++i)   // a sized and warmed context first
+        if (g_pool[i]->full) {
+            Ctx* t = g_pool[i];
+            g_pool[i] = g_pool[g_pool_n - 1];
+            g_pool[g_pool_n - 1] = t;
+            break;
+        }
     Ctx* c = g_pool_n ? g_pool[--g_pool_n] : nullptr;
     pthread_mutex_unlock(&g_pool_m);
     return c;

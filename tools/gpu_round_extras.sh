@@ -9,6 +9,10 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 hostname > $O/host_extras.txt
 fatal() { case $1 in 124|134|137|139) exit $1;; esac; }
+timeout -k 10 300 python -u -m pytest $R/tests/test_e2e_server.py -m gpu -s -q --timeout 240 --timeout-method thread > $O/e2e_extras.log 2>&1
+rc=$?; echo "e2e rc=$rc" >> $O/status_extras; fatal $rc
+E2E_TRACE_KEEP=$O/traces timeout -k 10 300 python -u $R/tools/e2e_trace.py > $O/e2e_trace.json 2> $O/e2e_trace.err
+rc=$?; echo "e2e_trace rc=$rc" >> $O/status_extras; fatal $rc
 bash $R/tools/gpu_sq_kinds.sh ${TAG}_sq k64_zero k64_random k64_runs50 k64_runs90 cfg1
 rc=$?; echo "sq rc=$rc" >> $O/status_extras; fatal $rc
 for S in 0 1; do
