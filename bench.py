@@ -411,11 +411,26 @@ class Loop:
     """The timed loop of one rank: `steps(k)` issues k steps (eager), or replays a captured graph
     of k steps (Exchange mode "graph").  In graph mode step i encodes into clens[i % 2]; the gather of
     step i runs on a branch, beside decode i and encode i + 1, and encode i + 2 (which rewrites
-    clens[i % 2]) waits for it."""
+    clens[i % 2]) waits for it.  Without an exchange (one rank), `plain` captures the k steps
+    (encode i, decode i, one after another on one stream) in one HIP graph as well, so the timed
+    region replays the launches instead of issuing 2k of them from Python (RLE_BENCH_GRAPH=0: eager)."""
 
     def __init__(self, B, xch, stream, dry):
         self.B, self.xch, self.stream, self.dry = B, xch, stream, dry
         self.graphs = {}
+        self.plain = (xch is None and not dry and os.environ.get("RLE_BENCH_GRAPH", "1") != "0")
+
+    def capture_plain(self, k):
+        g = torch.cuda.CUDAGraph()
+        main = torch.cuda.Stream(device=self.stream.device)
+        main.wait_stream(self.stream)
+        with torch.cuda.graph(g, stream=main):
+            for i in range(k):
+                self.B.encode(main, i % 2)
+                self.B.decode(main, i % 2)
+        self.stream.wait_stream(main)
+        torch.cuda.synchronize()
+        self.graphs[k] = g
 
     def one_step(self, slot):
         if self.xch is not None and self.xch.mode == "torch" and not self.dry:
@@ -454,6 +469,11 @@ class Loop:
         self.graphs[k] = g
 
     def steps(self, k):
+        if self.plain:
+            if k not in self.graphs:
+                self.capture_plain(k)
+            self.graphs[k].replay()
+            return
         if self.xch is not None and self.xch.mode == "graph":
             if k not in self.graphs:
                 self.capture(k)
@@ -533,6 +553,15 @@ def run_rank(args):
         if not graph_ok:
             xch.mode = "inline"
             loop.graphs.clear()
+    if loop.plain:   # (captured here, outside the timed region)
+        try:
+            loop.capture_plain(args.steps)
+            if args.warmup != args.steps:
+                loop.capture_plain(max(1, args.warmup))
+        except Exception as e:
+            print(f"graph capture failed ({e}); eager steps", file=sys.stderr)
+            loop.plain = False
+            loop.graphs.clear()
     loop.steps(max(1, args.warmup))
 
     if multi:
@@ -595,7 +624,10 @@ def run_rank(args):
                "config": {"workload": wl["desc"], "buffers_per_gpu": wl["n"],
                           "buffer_bytes": wl["size"] or "mixed 4 KiB-2 MiB",
                           "u_bytes_per_gpu": total_u // world, "c_bytes_rank0": c_bytes, "parallelism": par},
-               "verified_bit_exact_roundtrip": ok, "host_wait": sched, "kernels": kern, "roofline": roofline,
+               "verified_bit_exact_roundtrip": ok, "host_wait": sched,
+               "issue": ("one HIP graph of the K timed steps (captured before the timed region), replayed"
+                         if loop.plain else "eager: 2 launches per step from the host"),
+               "kernels": kern, "roofline": roofline,
                "cpu_baseline": cpu, "north_star_dec64k": north, "concurrent_streams": conc}
         if xch is not None:
             out["exchange"] = {"mode": xch.mode, "offsets_match_process_group": offsets_ok, "graph_captured": graph_ok,
