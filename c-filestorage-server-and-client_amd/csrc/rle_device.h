@@ -1433,7 +1433,22 @@ __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, 
     r.ta = lds_entry(tbase + (r.xa >> 4));
     r.tb = lds_entry(tbase + (r.xb >> 4));
     const u32 map = __builtin_amdgcn_perm(r.tb.y, r.tb.y, r.ta.y);
-    r.incl = (RLE_ABL & 1) ? map : wave_scan_incl(map, kMapId, OpMap());
+    // The scan composes the lanes' maps.  Where every owned lane's map is constant (its three entry
+    // phases reach one common token start inside the lane: nearly every lane of random, text-like
+    // and run-heavy streams, since a byte that differs from the two before it always starts a
+    // token), the composition up to lane l is lane l's own map, and the scan is skipped (the same
+    // values on lanes 0..62; lane 63's incl, which no consumer reads, is then its own map).  Streams
+    // whose lanes keep the phase open (a run of one digit-like byte) take the scan.  As the encode
+    // tile's run-start scan (enc_analyze_bounds).
+#ifndef RLE_DEC_MAPSKIP
+#define RLE_DEC_MAPSKIP 1
+#endif
+    constexpr uint64_t kOwnedLanes = (1ull << kOwnLanes) - 1ull;
+    if (RLE_ABL & 1) r.incl = map;
+    else if (RLE_DEC_MAPSKIP &&
+             !(__builtin_amdgcn_ballot_w64(map != __builtin_amdgcn_perm(map, map, 0x03000000u)) & kOwnedLanes))
+        r.incl = map;
+    else r.incl = wave_scan_incl(map, kMapId, OpMap());
     r.excl = from_prev_lane(r.incl, kMapId);
     return r;
 }
