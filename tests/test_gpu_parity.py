@@ -431,3 +431,33 @@ def test_uniform_tiles(seg):
     for i in range(len(streams)):
         ref, _ = O.decode(streams[i], us[i], us[i])
         assert dec[i] == ref, i
+
+
+@pytest.mark.parametrize("form", ["wave", "seg", "coop"])
+def test_phase_map_scan_skip_edges(form):
+    """The decode tile skips its phase-map scan when every owned lane's map is constant
+    (rle_device.h dec_prepare, RLE_DEC_MAPSKIP).  Streams of "k k k" tokens (a run of k copies of the
+    digit k: '2' x 2, '3' x 3, ...) keep the token phase open, so lanes inside such a stretch have
+    non-constant maps and the tile takes the scan.  Stretches of 1..400 tokens at every offset
+    around lane and tile edges, between random and run-heavy data, decoded in every form (one wave
+    per buffer, segmented, cooperative)."""
+    def stretch(ntok, first):
+        out, k = b"", first
+        for _ in range(ntok):
+            out += bytes([0x30 + k]) * k
+            k = 2 if k == 9 else k + 1
+        return out
+    xs = []
+    for off in list(range(0, 40)) + [1005, 1006, 1007, 1008, 1009, 2015, 2016, 3023, 3024]:
+        for ntok in (1, 5, 6, 11, 21, 22, 64, 400):
+            xs.append(O.gen(1, off, off) + stretch(ntok, 2 + off % 8) + O.gen(2, ntok, 700) + stretch(ntok // 2 + 1, 5))
+    ys = [O.encode(x) for x in xs]
+    if form == "coop":
+        dec, st = gpu_decode(ys, [len(x) for x in xs], max_in_len=max(len(y) for y in ys),
+                             max_out_len=max(len(x) for x in xs))
+    else:
+        dec, st = gpu_decode(ys, [len(x) for x in xs], seg=(form == "seg"))
+    assert (st == 0).all()
+    assert dec == xs
+    enc, st = gpu_encode(xs, seg=(form == "seg"))
+    assert (st == 0).all() and enc == ys
