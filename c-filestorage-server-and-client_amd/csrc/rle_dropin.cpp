@@ -902,7 +902,13 @@ bool svc_on(Ctx* c) {
     if (room) g_svc_ctx[g_svc_n++] = c;
     pthread_mutex_unlock(&g_svc_m);
     if (!room) return false;
-    if (hipStreamCreateWithFlags(&c->svc_s, hipStreamNonBlocking) != hipSuccess) {
+    // The service stream at the greatest priority: the runtime serves each priority from its own
+    // hardware queues, so the resident workgroup never shares a queue with the contexts' normal
+    // streams, whose dependent launches (a call's second kernel waits for its first) would otherwise
+    // wait behind it until it idles out (tools/probes/queue_probe.hip).
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&c->svc_s, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         (void)hipGetLastError();
         c->svc_s = nullptr;
         return false;   // (stays registered: svc_stop skips a context without a stream)

@@ -32,9 +32,14 @@ int main() {
     printf("{\"priority_range\": [%d, %d]}\n", lo, hi);
     uint32_t* d = nullptr;
     if (hipMalloc(&d, 4096) != hipSuccess) return 1;
-    for (int variant = 0; variant < 2; ++variant) {
+    // variants: the spinner at the greatest / least / the default priority (the normal streams' own);
+    // `dep`: each normal stream launches two tiny kernels back to back (the second waits for the first
+    // in its stream), as the drop-in's multi-launch calls do, instead of one
+    const int prios[3] = {hi, lo, 0};
+    for (int variant = 0; variant < 6; ++variant) {
+        const int prio = prios[variant % 3];   // hi = the greatest priority (numerically lowest)
+        const bool dep = variant >= 3;
         hipStream_t sp;
-        const int prio = variant == 0 ? hi : lo;   // hi = the greatest priority (numerically lowest)
         if (hipStreamCreateWithPriority(&sp, hipStreamNonBlocking, prio) != hipSuccess) return 1;
         hipStream_t s[12];
         for (int i = 0; i < 12; ++i)
@@ -45,15 +50,18 @@ int main() {
         const double t0 = now_ms();
         spin_kernel<<<1, 64, 0, sp>>>((uint64_t)(spin_ms * 100000.0));   // 100 MHz ticks
         double done[12];
-        for (int i = 0; i < 12; ++i) tiny_kernel<<<1, 64, 0, s[i]>>>(d + 64 * i);
+        for (int i = 0; i < 12; ++i) {
+            tiny_kernel<<<1, 64, 0, s[i]>>>(d + 64 * i);
+            if (dep) tiny_kernel<<<1, 64, 0, s[i]>>>(d + 64 * i);
+        }
         for (int i = 0; i < 12; ++i) {
             (void)hipStreamSynchronize(s[i]);
             done[i] = now_ms() - t0;
         }
         (void)hipStreamSynchronize(sp);
         const double spin_done = now_ms() - t0;
-        printf("{\"spinner_priority\": %d, \"spin_ms\": %.1f, \"spinner_done_ms\": %.2f, \"tiny_done_ms\": [", prio, spin_ms,
-               spin_done);
+        printf("{\"spinner_priority\": %d, \"dependent_pair\": %s, \"spin_ms\": %.1f, \"spinner_done_ms\": %.2f, \"tiny_done_ms\": [",
+               prio, dep ? "true" : "false", spin_ms, spin_done);
         for (int i = 0; i < 12; ++i) printf("%s%.2f", i ? ", " : "", done[i]);
         printf("]}\n");
         fflush(stdout);
