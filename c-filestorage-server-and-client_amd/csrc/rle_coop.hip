@@ -348,84 +348,58 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
 }
 
 // ================================================================ resident small-call service
-// (rle_service.h): one launch per busy period serves every thread context of the device.  Workgroup
-// g polls slots g, g + kSvcGroups, ... (wave 0, lane j: slot j's sequence word, one system-scope
-// load over PCIe per slot and poll); for a new request it fences (acquire, system scope, once per
-// request) and reads the slot's request line again -- the host writes the line and then the
-// sequence word, so a read ordered after seeing the new sequence returns the whole new line -- and
-// all kSvcWaves waves serve it with the barrier-uniform codec bodies on the slot's buffers; every
-// wave waits for its stores, and after a barrier thread 0 releases them at system scope and stores
-// the acknowledgement.  Leaving is collective (SvcState in device memory): kSvcIdleUs after the
-// latest request any workgroup served, kSvcLifeUs after the launch, on the stop word, or after
-// kSvcMaxPolls polls, a workgroup raises `exiting`; every workgroup that sees it leaves, and the
-// last one out stores `gone` with the launch's generation.  Mailbox words are read only with
-// vector loads (never the scalar cache).
+// (rle_service.h): one workgroup per drop-in thread context.  Wave 0 polls the context's mailbox
+// line (lanes 0..15: one 64-byte read over PCIe with system-scope loads; an acquire fence once a
+// request is seen);
+// a new complete request (req != done, tail == req) is broadcast through LDS and served by all
+// kSvcWaves waves with the barrier-uniform codec bodies on the context's mapped buffer; every wave
+// waits for its stores, and after a barrier thread 0 releases them at system scope and stores the
+// acknowledgement.  kSvcIdleUs after the last request, kSvcLifeUs after the launch, on the stop
+// word, or after kSvcMaxPolls polls, thread 0 marks `gone` with the launch's generation and the
+// workgroup ends.  Mailbox words are read only with vector loads (never the scalar cache).
 constexpr u32 kSvcUmax = 16384;
 constexpr u32 kSvcMaxPolls = 1u << 24;
-__global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcRegion* rg, SvcState* st, uint32_t gen,
-                                                              uint64_t idle_ticks, uint64_t life_ticks) {
-    __shared__ u32 done[kSvcPerGroup];   // latest sequence served per slot of this workgroup
-    __shared__ u32 sh[16];               // 0: action (0 none, 1 serve, 2 exit); 1: slot j; 4..15: line words 0..11
+__global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcMail* mb, const uint8_t* src, uint8_t* dst,
+                                                              uint32_t gen, uint32_t done, uint64_t idle_ticks,
+                                                              uint64_t life_ticks) {
+    __shared__ u32 sh[8];   // 0: action (0 none, 1 serve, 2 exit); 1..7: words 1..7 of the line (7: tail = req)
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = coop_wave();
-    const u32 g = blockIdx.x;
     const uint64_t t0 = wall_clock64();
     uint64_t last = t0;
-    if (wid == 0u && lane < kSvcPerGroup)
-        done[lane] = __hip_atomic_load(&rg->slot[g + kSvcGroups * lane].a.ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
+    const uint32_t* line = reinterpret_cast<const uint32_t*>(&mb->r);
     for (u32 polls = 0;; ++polls) {
         if (wid == 0u) {
-            const u32 ns = __hip_atomic_load(&rg->head.nslots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            const u32 s = g + kSvcGroups * lane;
-            const bool mine = lane < kSvcPerGroup && s < ns && s < kSvcSlots;
-            const u32 req = mine ? __hip_atomic_load(&rg->slot[s].r.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-            const uint64_t pm = __builtin_amdgcn_ballot_w64(mine && req != done[lane < kSvcPerGroup ? lane : 0u]);
+            const u32 w = lane < 16u ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+            const u32 req = readlane(w, 0), tail = readlane(w, 7), stop = readlane(w, 6);
             const uint64_t now = wall_clock64();
-            u32 act = 0u, js = 0u;
-            if (pm) {
-                js = (u32)__builtin_ctzll(pm);
+            u32 act = 0u;
+            u32 wl = w;
+            if (req != done && tail == req) {
                 // acquire once per request, not per poll (a system-scope acquire invalidates the
-                // XCD's L2: per poll, resident workgroups slowed every other's request, r4f)
+                // XCD's L2: per poll, 8 resident workgroups slowed every other's request, r4f)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 act = 1u;
                 last = now;
-                const uint32_t* line = reinterpret_cast<const uint32_t*>(&rg->slot[g + kSvcGroups * js].r);
-                const u32 w = lane < 12u ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-                if (lane < 12u) sh[4u + lane] = w;
-                if (lane == js) done[js] = req;   // (the line's req: the host posts one request per slot at a time)
-            } else if (__hip_atomic_load(&st->exiting, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                // the line again, ordered after seeing its new sequence number: the host writes the
+                // fields before `tail` and `req`, but the lanes' loads of one poll are not ordered
+                // among themselves, so a field read by another lane may predate them
+                wl = lane < 8u ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+            } else if (stop || now - last > idle_ticks || now - t0 > life_ticks || polls > kSvcMaxPolls) {
                 act = 2u;
-            } else {
-                const uint64_t lg = __hip_atomic_load(&st->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t l = lg > last ? lg : last;
-                const u32 stop = __hip_atomic_load(&rg->head.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (stop || now - l > idle_ticks || now - t0 > life_ticks || polls > kSvcMaxPolls) {
-                    if (lane == 0u) __hip_atomic_store(&st->exiting, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    act = 2u;
-                }
             }
-            if (lane == 0u) {
-                sh[0] = act;
-                sh[1] = js;
-            }
+            if (lane < 8u) sh[lane] = lane == 0u ? act : wl;
+            if (act == 1u) done = req;
         }
         __syncthreads();
         const u32 act = uniform(sh[0]);
         if (act == 2u) {
-            if (threadIdx.x == 0) {
-                const u32 out = __hip_atomic_fetch_add(&st->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (out + 1u == gridDim.x)
-                    __hip_atomic_store(&rg->gone.gone, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            if (threadIdx.x == 0) __hip_atomic_store(&mb->a.gone, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         if (act == 1u) {
-            SvcMail* mb = &rg->slot[g + kSvcGroups * uniform(sh[1])];
-            const u32 seq = uniform(sh[4]), op = uniform(sh[5]), in_len = uniform(sh[6]), out_len = uniform(sh[7]);
-            const u32 cap = uniform(sh[8]), wt = uniform(sh[9]) & kLaunchWt;
-            const uint8_t* src = reinterpret_cast<const uint8_t*>((uint64_t)uniform(sh[12]) | ((uint64_t)uniform(sh[13]) << 32));
-            uint8_t* dst = reinterpret_cast<uint8_t*>((uint64_t)uniform(sh[14]) | ((uint64_t)uniform(sh[15]) << 32));
+            const u32 seq = uniform(sh[7]), op = uniform(sh[1]), in_len = uniform(sh[2]);
+            const u32 out_len = uniform(sh[3]), cap = uniform(sh[4]), wt = uniform(sh[5]) & kLaunchWt;
             if (op == kSvcEncode) {
                 enc_coop_body<kSvcWaves, true>(src, dst, in_len, &mb->a.res_len, &mb->a.status, 0u, wt);
             } else {
@@ -436,7 +410,6 @@ __global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcRegion* rg, Sv
             if (threadIdx.x == 0) {   // ... then one system-scope release of them all and the acknowledgement
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                 __hip_atomic_store(&mb->a.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_fetch_max(&st->last, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         } else {
             __syncthreads();   // (wave 0 rewrites sh at the next poll)
@@ -566,14 +539,15 @@ extern "C" int rle_mi355x_set_coop_mode(int mode) {
     return RLE_OK;
 }
 
-// The resident small-call service of a device (rle_service.h; launched by csrc/rle_dropin.cpp
-// svc_ensure): kSvcGroups workgroups of kSvcWaves waves on the given stream, serving the slots of the
-// mapped region d_region (device address); d_state: the launch's SvcState, zeroed by the caller.
-extern "C" int rle_service_launch(void* d_region, void* d_state, uint32_t gen, void* stream) {
-    if (!d_region || !d_state) return RLE_E_INVAL;
+// The resident small-call service of one drop-in thread context (rle_service.h; launched by
+// csrc/rle_dropin.cpp svc_ensure): one workgroup of kSvcWaves waves on the given stream, serving
+// requests on the context's mapped buffer (d_src: input, d_dst: output) from sequence `done` on.
+extern "C" int rle_service_launch(void* d_mail, const void* d_src, void* d_dst, uint32_t gen, uint32_t done,
+                                  void* stream) {
+    if (!d_mail || !d_src || !d_dst) return RLE_E_INVAL;
     const uint64_t tick_per_us = 100;   // wall_clock64: 100 MHz
-    hipLaunchKernelGGL(rle::svc_kernel, dim3(rle::kSvcGroups), dim3(rle::kWave * rle::kSvcWaves), 0,
-                       (hipStream_t)stream, (rle::SvcRegion*)d_region, (rle::SvcState*)d_state, gen,
+    hipLaunchKernelGGL(rle::svc_kernel, dim3(1), dim3(rle::kWave * rle::kSvcWaves), 0, (hipStream_t)stream,
+                       (rle::SvcMail*)d_mail, (const uint8_t*)d_src, (uint8_t*)d_dst, gen, done,
                        tick_per_us * rle::kSvcIdleUs, tick_per_us * rle::kSvcLifeUs);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }

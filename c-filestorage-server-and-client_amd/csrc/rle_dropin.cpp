@@ -195,9 +195,12 @@ struct Ctx {
     uint8_t* h_cw = nullptr;                         // mapped launch words of combined launches (submit)
     uint8_t* d_cw = nullptr;
     uint32_t polled = 0;                             // polled launches since the last stream synchronize
-    int svc = -2;                                    // resident service (rle_service.h): its slot, -1 off, -2 not yet asked
-    rle::SvcMail* svc_h = nullptr;                   // the slot's mailbox (in the device's mapped service region)
+    int svc = -2;                                    // resident service (rle_service.h): 1 on, -1 off, -2 not yet asked
+    rle::SvcMail* svc_h = nullptr;                   // its mailbox (in the mapped zero-copy buffer) ...
+    rle::SvcMail* svc_d = nullptr;                   // ... and the mailbox's device address
+    hipStream_t svc_s = nullptr;                     // the service's stream
     uint32_t svc_seq = 0;                            // latest request
+    uint32_t svc_gen = 0;                            // latest launch (0: none)
     bool full = false;                               // presized and warmed for large calls (preinit)
 };
 // h_meta / d_meta regions, one per launch that can be in flight on the stream at once:
@@ -213,7 +216,8 @@ pthread_mutex_t g_exit_lock = PTHREAD_MUTEX_INITIALIZER;
 bool g_exiting = false;
 void preinit_join();   // below
 void svc_stop();   // below
-void svc_release(Ctx* c);
+void svc_end(Ctx* c);
+void svc_unregister(Ctx* c);
 void on_exit_handler() {
     preinit_join();   // (when called from the start-up thread's own exit: never; it makes no exit call)
     svc_stop();
@@ -231,7 +235,8 @@ void free_ctx(void* p) {
         return;
     }
     (void)hipSetDevice(c->dev);
-    svc_release(c);
+    svc_end(c);
+    svc_unregister(c);
     if (c->s) (void)hipStreamSynchronize(c->s);
     (void)hipHostFree(c->h_in);
     (void)hipHostFree(c->h_out);
@@ -875,120 +880,87 @@ uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
 }
 
 // ---------------------------------------------------------------- resident small-call service
-// (rle_service.h): one service per device for every thread context, each context with its own
-// mailbox slot in the device's mapped region.  The service runs on one stream at the greatest
-// priority, launched when a request finds it gone; g_svc[dev].m orders the launches and the slot
-// registry.
-extern "C" int rle_service_launch(void* d_region, void* d_state, uint32_t gen, void* stream);
-constexpr int kSvcDevices = 16;
-struct SvcDev {
-    pthread_mutex_t m = PTHREAD_MUTEX_INITIALIZER;
-    int state = 0;                        // 0 not set up, 1 ready, -1 unavailable
-    rle::SvcRegion* h = nullptr;          // mapped region ...
-    rle::SvcRegion* d = nullptr;          // ... and its device address
-    rle::SvcState* st = nullptr;          // device memory, zeroed before each launch
-    hipStream_t s = nullptr;
-    uint32_t gen = 0;                     // latest launch (0: none)
-    uint64_t used[rle::kSvcSlots / 64] = {};
-};
-SvcDev g_svc[kSvcDevices];
+// (rle_service.h): one resident workgroup per thread context, on the context's own service stream,
+// its mailbox in the context's mapped buffer.  g_svc_m guards the registry of contexts with a
+// service, which process exit stops (svc_stop).
+extern "C" int rle_service_launch(void* d_mail, const void* d_src, void* d_dst, uint32_t gen, uint32_t done,
+                                  void* stream);
+constexpr size_t kZcMail = kZcWords + 2048;   // the mailbox's offset in the mapped buffer (64-byte aligned)
+constexpr int kSvcMax = 256;                  // contexts with a service at once (the rest launch per call)
+pthread_mutex_t g_svc_m = PTHREAD_MUTEX_INITIALIZER;
+Ctx* g_svc_ctx[kSvcMax];
+int g_svc_n = 0;
 
-// Sets up device dev's service region and stream (once; under d.m).
-bool svc_dev_ready(SvcDev& d) {
-    if (d.state) return d.state > 0;
-    d.state = -1;
-    void* h = nullptr;
-    if (hipHostMalloc(&h, sizeof(rle::SvcRegion), hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+// Whether context c serves its small calls through its resident service (set up on first use).
+bool svc_on(Ctx* c) {
+    if (c->svc != -2) return c->svc > 0;
+    c->svc = -1;
+    if (!g_service) return false;
+    zc(c);
+    pthread_mutex_lock(&g_svc_m);
+    const bool room = g_svc_n < kSvcMax;
+    if (room) g_svc_ctx[g_svc_n++] = c;
+    pthread_mutex_unlock(&g_svc_m);
+    if (!room) return false;
+    // The service stream at the greatest priority: the runtime serves each priority from its own
+    // hardware queues, so the resident workgroup never shares a queue with the contexts' normal
+    // streams, whose dependent launches (a call's second kernel waits for its first) would otherwise
+    // wait behind it until it idles out (tools/probes/queue_probe.hip).
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&c->svc_s, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        c->svc_s = nullptr;
+        return false;   // (stays registered: svc_stop skips a context without a stream)
     }
-    memset(h, 0, sizeof(rle::SvcRegion));
-    void* dp = nullptr;
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess || hipMalloc((void**)&d.st, sizeof(rle::SvcState)) != hipSuccess ||
-        hipStreamCreateWithPriority(&d.s, hipStreamNonBlocking, hi) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;   // (the pieces made so far are kept until exit; the contexts launch per call)
-    }
-    d.h = static_cast<rle::SvcRegion*>(h);
-    d.d = static_cast<rle::SvcRegion*>(dp);
-    d.state = 1;
+    c->svc_h = reinterpret_cast<rle::SvcMail*>(c->h_zc + kZcMail);
+    c->svc_d = reinterpret_cast<rle::SvcMail*>(c->d_zc + kZcMail);
+    memset(c->svc_h, 0, sizeof(rle::SvcMail));
+    c->svc = 1;
     return true;
 }
-// Whether context c serves its small calls through the service (a slot taken on first use).
-bool svc_on(Ctx* c) {
-    if (c->svc != -2) return c->svc >= 0;
-    c->svc = -1;
-    if (!g_service || c->dev < 0 || c->dev >= kSvcDevices) return false;
-    zc(c);
-    SvcDev& d = g_svc[c->dev];
-    pthread_mutex_lock(&d.m);
-    int slot = -1;
-    if (svc_dev_ready(d))
-        for (int i = 0; i < (int)rle::kSvcSlots; ++i)
-            if (!((d.used[i / 64] >> (i % 64)) & 1u)) {
-                d.used[i / 64] |= 1ull << (i % 64);
-                slot = i;
-                break;
-            }
-    if (slot >= 0) {
-        rle::SvcMail* mb = &d.h->slot[slot];
-        c->svc_seq = __atomic_load_n(&mb->a.ack, __ATOMIC_ACQUIRE);   // a reused slot: its sequence goes on
-        mb->r.src = reinterpret_cast<uint64_t>(c->d_zc + kZcIn);
-        mb->r.dst = reinterpret_cast<uint64_t>(c->d_zc + kZcOut);
-        if ((uint32_t)slot >= __atomic_load_n(&d.h->head.nslots, __ATOMIC_ACQUIRE))
-            __atomic_store_n(&d.h->head.nslots, (uint32_t)slot + 1u, __ATOMIC_RELEASE);
-        c->svc_h = mb;
-        c->svc = slot;
-    }
-    pthread_mutex_unlock(&d.m);
-    return slot >= 0;
-}
-// A running service for a request just posted: launch one when there is none or the last has ended
-// (wait for that launch to complete first).  Under d.m, so one thread relaunches.
+// A running service for c's request just posted: launch one when there is none or the last has ended
+// (wait for that launch to complete first).
 void svc_ensure(Ctx* c) {
-    SvcDev& d = g_svc[c->dev];
-    const uint32_t gen = __atomic_load_n(&d.gen, __ATOMIC_ACQUIRE);
-    if (gen && __atomic_load_n(&d.h->gone.gone, __ATOMIC_ACQUIRE) != gen) return;
-    pthread_mutex_lock(&d.m);
-    if (!d.gen || __atomic_load_n(&d.h->gone.gone, __ATOMIC_ACQUIRE) == d.gen) {
-        if (d.gen) check(hipStreamSynchronize(d.s), "hipStreamSynchronize(service)");
-        check(hipMemsetAsync(d.st, 0, sizeof(rle::SvcState), d.s), "hipMemsetAsync(service state)");
-        if (rle_service_launch(d.d, d.st, d.gen + 1u, d.s) != RLE_OK) die("service launch", hipGetLastError());
-        __atomic_store_n(&d.gen, d.gen + 1u, __ATOMIC_RELEASE);
-    }
-    pthread_mutex_unlock(&d.m);
+    if (c->svc_gen && __atomic_load_n(&c->svc_h->a.gone, __ATOMIC_ACQUIRE) != c->svc_gen) return;
+    if (c->svc_gen) check(hipStreamSynchronize(c->svc_s), "hipStreamSynchronize(service)");
+    const uint32_t done = __atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE);
+    if (rle_service_launch(c->svc_d, c->d_zc + kZcIn, c->d_zc + kZcOut, c->svc_gen + 1u, done, c->svc_s) != RLE_OK)
+        die("service launch", hipGetLastError());
+    ++c->svc_gen;
 }
-// Context c gives its slot back (thread exit).  Its last request was acknowledged (calls wait for
-// it), so the service holds nothing of c's.
-void svc_release(Ctx* c) {
-    if (c->svc < 0) return;
-    SvcDev& d = g_svc[c->dev];
-    pthread_mutex_lock(&d.m);
-    d.used[c->svc / 64] &= ~(1ull << (c->svc % 64));
-    pthread_mutex_unlock(&d.m);
+// End c's service and wait for it (thread exit, process exit).
+void svc_end(Ctx* c) {
+    if (c->svc <= 0 || !c->svc_s) return;
+    if (c->svc_gen) {
+        __atomic_store_n(&c->svc_h->r.stop, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(c->svc_s);
+    }
+    (void)hipStreamDestroy(c->svc_s);
+    c->svc_s = nullptr;
     c->svc = -1;
-    c->svc_h = nullptr;
 }
-// At exit (on_exit_handler, before the runtime's teardown): every device's service ends.
-void svc_stop() {
-    for (int i = 0; i < kSvcDevices; ++i) {
-        SvcDev& d = g_svc[i];
-        pthread_mutex_lock(&d.m);
-        if (d.state > 0 && d.gen) {
-            __atomic_store_n(&d.h->head.stop, 1u, __ATOMIC_RELEASE);
-            int cur = 0;
-            if (hipGetDevice(&cur) == hipSuccess && cur != i) (void)hipSetDevice(i);
-            (void)hipStreamSynchronize(d.s);
-            if (cur != i) (void)hipSetDevice(cur);
+void svc_unregister(Ctx* c) {
+    pthread_mutex_lock(&g_svc_m);
+    for (int i = 0; i < g_svc_n; ++i)
+        if (g_svc_ctx[i] == c) {
+            g_svc_ctx[i] = g_svc_ctx[--g_svc_n];
+            break;
         }
-        pthread_mutex_unlock(&d.m);
-    }
+    pthread_mutex_unlock(&g_svc_m);
+}
+// At exit (on_exit_handler, before the runtime's teardown): every service ends.
+void svc_stop() {
+    pthread_mutex_lock(&g_svc_m);
+    for (int i = 0; i < g_svc_n; ++i)
+        if (g_svc_ctx[i]->svc > 0 && g_svc_ctx[i]->svc_gen) __atomic_store_n(&g_svc_ctx[i]->svc_h->r.stop, 1u, __ATOMIC_RELEASE);
+    for (int i = 0; i < g_svc_n; ++i)
+        if (g_svc_ctx[i]->svc > 0 && g_svc_ctx[i]->svc_gen) (void)hipStreamSynchronize(g_svc_ctx[i]->svc_s);
+    pthread_mutex_unlock(&g_svc_m);
 }
 // One request on c's mapped buffer: returns the status, *res_len the encoded size.  The line is
-// written with the sequence number last; the wait polls ack, checking every 256 polls that the
-// service has not ended before taking the request.
+// written with the sequence number last (tail, then req); the wait polls ack, checking every 256
+// polls that the service has not ended before taking the request.
 uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64_t cap, uint64_t* res_len) {
     rle::SvcReq* r = &c->svc_h->r;
     r->op = op;
