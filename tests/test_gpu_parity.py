@@ -385,11 +385,13 @@ def test_large_batch_decode_plain_stores():
     assert dec2 == dec
 
 
-@pytest.mark.parametrize("n", [4097, 4099, 8195, 12288])
+@pytest.mark.parametrize("n", [4097, 4099, 8195, 12288, 16384, 16385])
 def test_decode_ragged_batches_past_one_round(n):
     """Batches just past one residency round of the chip (4096 waves): a last round of one to a few
     buffers, XCD-padding workgroups with no buffer, and long / short / serial buffers mixed --
-    each buffer decoded exactly once, bit-exact, every status written."""
+    each buffer decoded exactly once, bit-exact, every status written.  Up to 16384 buffers the
+    issue order is sorted without a memset (per-workgroup parts), from 16385 with the global
+    histogram (rle_kernels.hip dec_order_*)."""
     rng = np.random.default_rng(n)
     sizes = rng.integers(0, 3000, size=n)
     sizes[::7] = 20000   # a few long buffers, so ranges finish unevenly
