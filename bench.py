@@ -596,6 +596,21 @@ def run_rank(args):
     else:
         total_u = u_local
 
+    # the same K steps issued eagerly (2 launches per step from the host), right after the graph-
+    # replayed timed loop, so the headline's launch share is visible beside it
+    eager = None
+    if loop.plain:
+        loop.plain = False
+        loop.steps(max(1, args.warmup))
+        sync(dry)
+        t1 = time.perf_counter()
+        loop.steps(args.steps)
+        sync(dry)
+        te = time.perf_counter() - t1
+        loop.plain = True
+        eager = {"value": round(total_u * args.steps / te / GIB, 3), "ms_per_step": round(te / args.steps * 1e3, 4),
+                 "issue": "eager: 2 launches per step from the host, same batch, timed after the graph loop"}
+
     kern = roofline = conc = north = cpu = None
     if not dry:
         kern, roofline = measure_kernels(B, args, stream, u_local, c_bytes, loop_gpu_s)
@@ -627,6 +642,8 @@ def run_rank(args):
                "verified_bit_exact_roundtrip": ok, "host_wait": sched,
                "issue": ("one HIP graph of the K timed steps (captured before the timed region), replayed"
                          if loop.plain else "eager: 2 launches per step from the host"),
+               "value_eager": eager["value"] if eager else None,
+               "ms_per_step_eager": eager["ms_per_step"] if eager else None,
                "kernels": kern, "roofline": roofline,
                "cpu_baseline": cpu, "north_star_dec64k": north, "concurrent_streams": conc}
         if xch is not None:

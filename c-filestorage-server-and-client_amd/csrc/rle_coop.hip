@@ -347,6 +347,10 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     dec_coop_body<kW, kUmax, false>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
 }
 
+#ifndef RLE_VARIANTS
+#define RLE_VARIANTS 0
+#endif
+#if RLE_VARIANTS   // the resident service is built into the test library only (round 5)
 // ================================================================ resident small-call service
 // (rle_service.h): one workgroup per drop-in thread context.  Wave 0 polls the context's mailbox
 // line (lanes 0..15: one 64-byte read over PCIe with system-scope loads; an acquire fence once a
@@ -417,6 +421,7 @@ __global__ __launch_bounds__(kWave* kSvcWaves) void svc_kernel(SvcMail* mb, cons
         }
     }
 }
+#endif  // RLE_VARIANTS
 
 }  // namespace rle
 
@@ -539,6 +544,7 @@ extern "C" int rle_mi355x_set_coop_mode(int mode) {
     return RLE_OK;
 }
 
+#if RLE_VARIANTS
 // The resident small-call service of one drop-in thread context (rle_service.h; launched by
 // csrc/rle_dropin.cpp svc_ensure): one workgroup of kSvcWaves waves on the given stream, serving
 // requests on the context's mapped buffer (d_src: input, d_dst: output) from sequence `done` on.
@@ -551,3 +557,4 @@ extern "C" int rle_service_launch(void* d_mail, const void* d_src, void* d_dst, 
                        tick_per_us * rle::kSvcIdleUs, tick_per_us * rle::kSvcLifeUs);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
+#endif  // RLE_VARIANTS

@@ -19,6 +19,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <errno.h>
+#include <link.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -146,7 +147,7 @@ size_t g_presize = 1u << 20;   // staging allocated with each thread context (pr
 // launch).  RLE_MI355X_POLL=0: synchronize instead.
 bool g_poll = true;
 // Small calls through the resident service (rle_service.h) instead of a launch each:
-// RLE_MI355X_SERVICE=1 (off by default until measured).
+// RLE_MI355X_SERVICE=1, in the RLE_VARIANTS test library only (measured slower, round 5).
 bool g_service = false;
 // Zero-copy calls from this many bytes (encode: U, decode: C) run the segmented kernels on the mapped
 // buffer instead of one wave walking it, and the zero-copy form then takes calls up to 64 KiB in
@@ -172,8 +173,16 @@ size_t g_stage_cap = 32u << 20;
 #if RLE_TEST_HOOKS
 size_t g_fail_above = SIZE_MAX;
 inline bool injected_failure(size_t n) { return n > g_fail_above; }
+// RLE_MI355X_FAKE_DEVICES=<n> (CPU lifecycle tests, tests/test_lifecycle.py): the library believes n
+// devices exist and builds thread contexts that hold no HIP object (no HIP call is made for them),
+// so the start-up thread, the pool, the pthread-key destructors, fork and exit ordering all run on a
+// machine without a GPU, under ASan and TSan.  RLE_MI355X_FAKE_DELAY_US: each context takes that long.
+int g_fake_devs = 0;
+unsigned g_fake_delay_us = 0;
 #else
 constexpr bool injected_failure(size_t) { return false; }
+constexpr int g_fake_devs = 0;
+constexpr unsigned g_fake_delay_us = 0;
 #endif
 
 struct Ctx {
@@ -234,6 +243,11 @@ void free_ctx(void* p) {
         pthread_mutex_unlock(&g_exit_lock);
         return;
     }
+    if (g_fake_devs) {   // (test build: a context without HIP objects)
+        delete c;
+        pthread_mutex_unlock(&g_exit_lock);
+        return;
+    }
     (void)hipSetDevice(c->dev);
     svc_end(c);
     svc_unregister(c);
@@ -258,7 +272,12 @@ void free_ctx(void* p) {
 }
 
 void init_once() {
-    if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
+#if RLE_TEST_HOOKS
+    if (const char* e = getenv("RLE_MI355X_FAKE_DEVICES")) g_fake_devs = atoi(e) > 0 ? atoi(e) : 0;
+    if (const char* e = getenv("RLE_MI355X_FAKE_DELAY_US")) g_fake_delay_us = (unsigned)atoi(e);
+#endif
+    if (g_fake_devs) g_ndev = g_fake_devs;
+    else if (hipGetDeviceCount(&g_ndev) != hipSuccess) g_ndev = 0;
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
     if (const char* e = getenv("RLE_MI355X_POLL")) g_poll = strcmp(e, "0") != 0;
@@ -293,6 +312,11 @@ void warm_small(Ctx* c);   // below
 Ctx* new_ctx(int dev, bool sized = true) {
     Ctx* c = new Ctx();
     c->dev = dev;
+    if (g_fake_devs) {   // (test build: no HIP objects)
+        if (g_fake_delay_us) usleep(g_fake_delay_us);
+        c->full = sized;
+        return c;
+    }
     check(hipSetDevice(c->dev), "hipSetDevice");
     check(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking), "hipStreamCreate");
     if (hipMalloc(&c->d_meta, kMetaSlots * sizeof(uint64_t)) != hipSuccess ||
@@ -314,7 +338,9 @@ Ctx* new_ctx(int dev, bool sized = true) {
 // (stream, pinned and device buffers: hipHostMalloc costs milliseconds) and the first use of the copy
 // engines (e2e battery 1: 89-167 ms against the reference's 5-7 ms; ns_stage_in 7.75 ms for 883 KB).
 // Now the library's constructor starts one background thread when it is loaded, before main() runs
-// in a server that links it: the thread initialises the runtime and builds RLE_MI355X_PREINIT
+// in a server that links it (round 5: only a main program that names the library among its DT_NEEDED
+// entries, or any process with RLE_MI355X_PREINIT > 0; a process that dlopen()s it, such as Python,
+// does not start it unless asked): the thread initialises the runtime and builds RLE_MI355X_PREINIT
 // contexts (default 8; 0 = off, the round-3 behaviour) in two phases: first one sized and warmed
 // with one call of every transfer form (pinned, pageable) and kernel form, and the others only
 // ready for small calls (stream, launch words, zero-copy buffer, one small call each way), each put
@@ -361,7 +387,8 @@ void* preinit_main(void*) {
             // first uses (each kernel's first launch, the runtime's copy paths) are then done before
             // a worker's first large call (r4 e2e: with every context light first, the first large
             // calls spent 26.6 ms staging in against 0.07 ms)
-            if (i == 0) warm(c);
+            if (g_fake_devs) {
+            } else if (i == 0) warm(c);
             else warm_small(c);
         } catch (const std::bad_alloc&) {
             if (c) free_ctx(c);
@@ -392,9 +419,13 @@ void* preinit_main(void*) {
         if (!c) break;
         try {
             TraceScope ts('P', 2, 0, 0);   // (trace record: one context's phase-2 sizing and warm-up)
-            check(hipSetDevice(c->dev), "hipSetDevice");
-            presize(c);
-            warm(c);
+            if (g_fake_devs) {
+                if (g_fake_delay_us) usleep(g_fake_delay_us);
+            } else {
+                check(hipSetDevice(c->dev), "hipSetDevice");
+                presize(c);
+                warm(c);
+            }
         } catch (const std::bad_alloc&) {
         }
         c->full = true;   // (also after an allocation failure: not tried again)
@@ -419,11 +450,61 @@ void preinit_join() {
     if (g_pre_started.exchange(false)) pthread_join(g_pre_thread, nullptr);
 }
 void preinit_exit() { preinit_join(); }
+// Whether the main program itself names this library among its DT_NEEDED entries (the reference
+// server linked with -lrle_mi355x), as opposed to a process that dlopen()s it
+// (Python's ctypes: tests, bench.py, the torch binding).  Only such a program gets the background
+// start-up by default (loading the library from Python must not initialise the GPU, and
+// a multi-rank job must not build contexts on every rank's GPUs).
+int needed_by_main_cb(struct dl_phdr_info* info, size_t, void* out) {
+    const ElfW(Dyn)* dyn = nullptr;
+    for (int i = 0; i < info->dlpi_phnum; ++i)
+        if (info->dlpi_phdr[i].p_type == PT_DYNAMIC)
+            dyn = reinterpret_cast<const ElfW(Dyn)*>(info->dlpi_addr + info->dlpi_phdr[i].p_vaddr);
+    if (dyn) {
+        // the loader rewrites DT_STRTAB in place to an absolute address on x86-64; take the form that
+        // lies inside one of the object's loaded segments
+        uintptr_t strtab = 0;
+        for (const ElfW(Dyn)* d = dyn; d->d_tag != DT_NULL; ++d)
+            if (d->d_tag == DT_STRTAB) strtab = (uintptr_t)d->d_un.d_ptr;
+        auto inside = [&](uintptr_t a) {
+            for (int i = 0; i < info->dlpi_phnum; ++i) {
+                const ElfW(Phdr)& ph = info->dlpi_phdr[i];
+                const uintptr_t lo = info->dlpi_addr + ph.p_vaddr;
+                if (ph.p_type == PT_LOAD && a >= lo && a < lo + ph.p_memsz) return true;
+            }
+            return false;
+        };
+        if (strtab && !inside(strtab)) strtab += info->dlpi_addr;
+        if (strtab && inside(strtab))
+            for (const ElfW(Dyn)* d = dyn; d->d_tag != DT_NULL; ++d)
+                if (d->d_tag == DT_NEEDED && strstr(reinterpret_cast<const char*>(strtab + d->d_un.d_val), "librle_mi355x"))
+                    *static_cast<int*>(out) = 1;
+    }
+    return 1;   // the first object reported is the main program: stop there
+}
+bool needed_by_main() {
+    int found = 0;
+    dl_iterate_phdr(needed_by_main_cb, &found);
+    return found != 0;
+}
+// fork() while the start-up thread runs: the child has no such thread and no usable HIP state, so it
+// starts with an empty pool and no start-up in progress (pool_take would otherwise wait on a phase
+// that never ends).
+void preinit_atfork_prepare() { pthread_mutex_lock(&g_pool_m); }
+void preinit_atfork_parent() { pthread_mutex_unlock(&g_pool_m); }
+void preinit_atfork_child() {
+    g_pool_n = 0;
+    g_pre_running = g_pre_phase1 = false;
+    g_pre_started.store(false);
+    g_pre_stop.store(true);
+    pthread_mutex_unlock(&g_pool_m);
+}
 __attribute__((constructor)) void preinit_start() {
     if (const char* t = getenv("RLE_MI355X_TRACE"))
         if (*t) g_trace = static_cast<TraceRec*>(calloc(kTraceMax, sizeof(TraceRec)));
     const char* e = getenv("RLE_MI355X_PREINIT");
-    if (e && atoi(e) <= 0) return;
+    if (e ? atoi(e) <= 0 : !needed_by_main()) return;
+    pthread_atfork(preinit_atfork_prepare, preinit_atfork_parent, preinit_atfork_child);
     atexit(preinit_exit);
     pthread_mutex_lock(&g_pool_m);
     g_pre_running = g_pre_phase1 = true;
@@ -431,6 +512,12 @@ __attribute__((constructor)) void preinit_start() {
     else g_pre_running = g_pre_phase1 = false;
     pthread_mutex_unlock(&g_pool_m);
 }
+extern "C" int rle_mi355x_preinit_state(void) { return g_pre_started.load() ? 1 : 0; }
+#if RLE_TEST_HOOKS
+Ctx* ctx();   // below
+// Test build only: this thread's context (taken from the pool or made), its device.
+extern "C" int rle_test_touch_ctx(void) { return ctx()->dev; }
+#endif
 // A warm context from the pool, or nullptr (none left and the thread has finished).
 Ctx* pool_take() {
     pthread_mutex_lock(&g_pool_m);
@@ -451,7 +538,7 @@ Ctx* ctx() {
     pthread_once(&g_once, init_once);
     Ctx* c = static_cast<Ctx*>(pthread_getspecific(g_key));
     if (c) {
-        check(hipSetDevice(c->dev), "hipSetDevice");
+        if (!g_fake_devs) check(hipSetDevice(c->dev), "hipSetDevice");
         return c;
     }
     if (g_ndev <= 0) {
@@ -460,7 +547,7 @@ Ctx* ctx() {
     }
     const uint64_t t0 = g_trace ? now_ns() : 0;
     c = pool_take();
-    if (c) check(hipSetDevice(c->dev), "hipSetDevice");
+    if (c && !g_fake_devs) check(hipSetDevice(c->dev), "hipSetDevice");
     else c = new_ctx((g_dev_pin >= 0 && g_dev_pin < g_ndev) ? g_dev_pin : (int)(g_next_dev++ % (unsigned)g_ndev),
                      !g_pre_started.load());   // (beside the start-up thread: unsized, for a short first call)
     pthread_setspecific(g_key, c);
@@ -880,6 +967,10 @@ uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
 }
 
 // ---------------------------------------------------------------- resident small-call service
+// Measured slower than the per-call launches at 8 threads and behind the server (DESIGN.md §6,
+// profiles/r4r_callrate.txt, r4r_e2e_compare.json), so since round 5 it is built only into the
+// RLE_VARIANTS test library (RLE_MI355X_SERVICE=1 there); the product library carries stubs.
+#if RLE_VARIANTS
 // (rle_service.h): one resident workgroup per thread context, on the context's own service stream,
 // its mailbox in the context's mapped buffer.  g_svc_m guards the registry of contexts with a
 // service, which process exit stops (svc_stop).
@@ -921,13 +1012,16 @@ bool svc_on(Ctx* c) {
 }
 // A running service for c's request just posted: launch one when there is none or the last has ended
 // (wait for that launch to complete first).
-void svc_ensure(Ctx* c) {
-    if (c->svc_gen && __atomic_load_n(&c->svc_h->a.gone, __ATOMIC_ACQUIRE) != c->svc_gen) return;
+std::atomic<bool> g_svc_stopped{false};   // svc_stop ran: no service is launched again
+bool svc_ensure(Ctx* c) {
+    if (c->svc_gen && __atomic_load_n(&c->svc_h->a.gone, __ATOMIC_ACQUIRE) != c->svc_gen) return true;
+    if (g_svc_stopped.load(std::memory_order_acquire)) return false;
     if (c->svc_gen) check(hipStreamSynchronize(c->svc_s), "hipStreamSynchronize(service)");
     const uint32_t done = __atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE);
     if (rle_service_launch(c->svc_d, c->d_zc + kZcIn, c->d_zc + kZcOut, c->svc_gen + 1u, done, c->svc_s) != RLE_OK)
         die("service launch", hipGetLastError());
     ++c->svc_gen;
+    return true;
 }
 // End c's service and wait for it (thread exit, process exit).
 void svc_end(Ctx* c) {
@@ -951,6 +1045,7 @@ void svc_unregister(Ctx* c) {
 }
 // At exit (on_exit_handler, before the runtime's teardown): every service ends.
 void svc_stop() {
+    g_svc_stopped.store(true, std::memory_order_release);
     pthread_mutex_lock(&g_svc_m);
     for (int i = 0; i < g_svc_n; ++i)
         if (g_svc_ctx[i]->svc > 0 && g_svc_ctx[i]->svc_gen) __atomic_store_n(&g_svc_ctx[i]->svc_h->r.stop, 1u, __ATOMIC_RELEASE);
@@ -960,7 +1055,10 @@ void svc_stop() {
 }
 // One request on c's mapped buffer: returns the status, *res_len the encoded size.  The line is
 // written with the sequence number last (tail, then req); the wait polls ack, checking every 256
-// polls that the service has not ended before taking the request.
+// polls that the service has not ended before taking the request.  Once process exit has stopped
+// the services (svc_stop) a request that finds its service gone is not served: kSvcStopped, and the
+// caller takes the launch path (a relaunch would exit at once on the stop word).
+constexpr uint32_t kSvcStopped = 0xFFFFFFFFu;
 uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64_t cap, uint64_t* res_len) {
     rle::SvcReq* r = &c->svc_h->r;
     r->op = op;
@@ -971,13 +1069,13 @@ uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64
     const uint32_t seq = ++c->svc_seq;
     __atomic_store_n(&r->tail, seq, __ATOMIC_RELEASE);
     __atomic_store_n(&r->req, seq, __ATOMIC_RELEASE);
-    svc_ensure(c);
+    if (!svc_ensure(c)) return kSvcStopped;
     const uint64_t t0 = now_ns();
     bool yield = false;
     for (uint32_t i = 1;; ++i) {
         if (__atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE) == seq) break;
         if ((i & 255u) == 0u) {
-            svc_ensure(c);
+            if (!svc_ensure(c) && __atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE) != seq) return kSvcStopped;
             const uint64_t t = now_ns() - t0;
             if (t > 10000000000ull) die("service request (10 s)", hipErrorUnknown);
             yield = t > kSpinNs;
@@ -989,10 +1087,20 @@ uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64
     return __atomic_load_n(&c->svc_h->a.status, __ATOMIC_ACQUIRE);
 }
 
+#else
+constexpr uint32_t kSvcStopped = 0xFFFFFFFFu;
+inline bool svc_on(Ctx*) { return false; }
+inline uint32_t svc_call(Ctx*, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t*) { return kSvcStopped; }
+void svc_end(Ctx*) {}
+void svc_unregister(Ctx*) {}
+void svc_stop() {}
+#endif  // RLE_VARIANTS (resident service)
+
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, U);
     size_t C;
+    uint32_t st_svc = 0;
 #if RLE_VARIANTS
     if (g_coalesce) {
         Req r;
@@ -1012,9 +1120,8 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
         check_encode_status((uint32_t)hw[4]);
         C = hw[3];
-    } else if (svc_on(c)) {
-        uint64_t Cs = 0;
-        check_encode_status(svc_call(c, rle::kSvcEncode, U, 0, 0, &Cs));
+    } else if (uint64_t Cs = 0; svc_on(c) && (st_svc = svc_call(c, rle::kSvcEncode, U, 0, 0, &Cs)) != kSvcStopped) {
+        check_encode_status(st_svc);
         C = Cs;
     } else {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
@@ -1057,8 +1164,7 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
             die("decode launch", hipGetLastError());
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
         st = (uint32_t)hw[5];
-    } else if (svc_on(c)) {
-        st = svc_call(c, rle::kSvcDecode, C, U, total, nullptr);
+    } else if (svc_on(c) && (st = svc_call(c, rle::kSvcDecode, C, U, total, nullptr)) != kSvcStopped) {
     } else {
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = kPending;

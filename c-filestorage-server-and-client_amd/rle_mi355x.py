@@ -370,11 +370,30 @@ def _ws(ws):
     return (_ptr(ws), ws.numel() * ws.element_size()) if ws is not None else (None, 0)
 
 
+# Workspaces made for calls that pass none: the scan kernels run on `stream` (or the
+# comm stream, or a captured graph replays them) after the call returns, so a temporary torch tensor
+# could be handed to another tensor by the caching allocator while they still use it.  One workspace
+# per (device, n, stream, slot) instead, kept for the life of the process: calls on one stream run
+# in order, and calls that may run at once (different streams or slots) get different workspaces.
+_WS_CACHE = {}
+
+
+def _default_ws(n, device, stream, slot):
+    import torch
+    dev = torch.device(device)
+    key = (dev.type, dev.index, int(n), _stream_ptr(stream).value or 0, slot)
+    ws = _WS_CACHE.get(key)
+    if ws is None:
+        ws = _WS_CACHE[key] = dist_workspace(n, dev)
+    return ws
+
+
 def dist_gather_offsets(sizes, gathered, offsets, stream=None, ws=None):
     """One exchange step (rle_dist_gather_offsets) on `stream`: sizes (int64[n], device) all-gathered
-    and scanned into offsets (int64[world * n]) in the global stream order; ws: dist_workspace(n)."""
+    and scanned into offsets (int64[world * n]) in the global stream order; ws: dist_workspace(n)
+    (None: a workspace of this module's own for this stream, kept alive, _default_ws)."""
     if ws is None:
-        ws = dist_workspace(sizes.numel(), sizes.device)
+        ws = _default_ws(sizes.numel(), sizes.device, stream, "gather")
     _check(lib().rle_dist_gather_offsets(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets), *_ws(ws),
                                          _stream_ptr(stream)), "rle_dist_gather_offsets")
 
@@ -382,9 +401,9 @@ def dist_gather_offsets(sizes, gathered, offsets, stream=None, ws=None):
 def dist_gather_offsets_async(sizes, gathered, offsets, codec_stream, comm_stream, slot: int, ws=None):
     """The exchange on comm_stream after the work issued on codec_stream (rle_dist_gather_offsets_async);
     codec_stream waits only for the previous call's exchange (the other slot).  Slots must alternate;
-    ws: this slot's dist_workspace(n)."""
+    ws: this slot's dist_workspace(n) (None: this module's own for the comm stream and slot)."""
     if ws is None:
-        ws = dist_workspace(sizes.numel(), sizes.device)
+        ws = _default_ws(sizes.numel(), sizes.device, comm_stream, ("async", int(slot)))
     _check(lib().rle_dist_gather_offsets_async(_ptr(sizes), sizes.numel(), _ptr(gathered), _ptr(offsets), *_ws(ws),
                                                _stream_ptr(codec_stream), _stream_ptr(comm_stream), int(slot)),
            "rle_dist_gather_offsets_async")
@@ -392,7 +411,7 @@ def dist_gather_offsets_async(sizes, gathered, offsets, codec_stream, comm_strea
 
 def dist_offsets(gathered, world: int, n: int, offsets, stream=None, ws=None):
     if ws is None:
-        ws = dist_workspace(n, gathered.device)
+        ws = _default_ws(n, gathered.device, stream, "offsets")
     _check(lib().rle_dist_offsets_device(_ptr(gathered), world, n, _ptr(offsets), *_ws(ws), _stream_ptr(stream)),
            "rle_dist_offsets_device")
 

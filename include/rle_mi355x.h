@@ -215,6 +215,13 @@ int rle_mi355x_set_coop_mode(int mode);
  * times it as the practical HBM ceiling of SURVEY.md §8(d).  RLE_E_INVAL on bad sizes. */
 int rle_copy_device(void* d_dst, const void* d_src, uint64_t nbytes, void* stream);
 
+/* The drop-in's background start-up (HIP runtime, warm thread contexts) at library load: 1 when this
+ * process started it, 0 otherwise.  It starts in a program that links the library (the reference
+ * server, INTEGRATION.md §2: the library is among the main program's DT_NEEDED entries) or whenever
+ * RLE_MI355X_PREINIT > 0; a process that dlopen()s the library (Python ctypes) does no GPU work
+ * before its first codec call unless RLE_MI355X_PREINIT asks for it.  No reference interface. */
+int rle_mi355x_preinit_state(void);
+
 /* Number of visible HIP devices (0 when none). */
 int rle_mi355x_device_count(void);
 

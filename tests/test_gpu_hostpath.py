@@ -209,11 +209,14 @@ print("ok")
 def test_polled_small_calls_bit_exact(poll, service, zcseg):
     """The zero-copy small calls' completion: polling the status word the kernel stores behind a
     system-scope release (RLE_MI355X_POLL=1, the default) or hipStreamSynchronize (=0), or the
-    resident service (RLE_MI355X_SERVICE=1: no launch per call, csrc/rle_service.h).  600
+    resident service (RLE_MI355X_SERVICE=1: no launch per call, csrc/rle_service.h; built into the
+    RLE_VARIANTS test library only since round 5, so that case loads it).  600
     consecutive calls of 0-16 KiB (cooperative and one-wave kernels), decodes with an extra region,
     serial-path streams, then 8 threads x 150 round trips, all against the oracle.  zcseg: calls
     from that many bytes run the segmented kernels on the mapped buffer (RLE_MI355X_ZC_SEG)."""
     env = dict(os.environ, RLE_MI355X_POLL=poll, RLE_MI355X_SERVICE=service, RLE_MI355X_ZC_SEG=zcseg)
+    if service == "1":
+        env["RLE_MI355X_LIB"] = VARIANTS_LIB
     r = subprocess.run([sys.executable, "-c", _POLL_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
@@ -255,8 +258,9 @@ print("ok")
 def test_service_relaunch_and_overflow_bit_exact():
     """The resident service (RLE_MI355X_SERVICE=1) across its own idle exits (calls 3 ms apart: a
     relaunch each) and with 72 threads at once (72 resident workgroups, one per thread context),
-    every stream against the oracle; the process then exits with every service stopped."""
-    env = dict(os.environ, RLE_MI355X_SERVICE="1")
+    every stream against the oracle; the process then exits with every service stopped.  (The
+    service is built into the RLE_VARIANTS test library only.)"""
+    env = dict(os.environ, RLE_MI355X_SERVICE="1", RLE_MI355X_LIB=VARIANTS_LIB)
     r = subprocess.run([sys.executable, "-c", _SERVICE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])

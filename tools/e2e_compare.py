@@ -14,7 +14,6 @@ Batteries 1 and 2 are timed twice: from the moment the server's socket appears (
 calls may still wait for the drop-in's background start-up) and on a server that has been up for
 SETTLE seconds (started: a serving process).  Every returned file is checked byte for byte.
 server_gpu also runs with RLE_MI355X_PREINIT=0 (round 3's lazy start-up on the first call) and with
-RLE_MI355X_SERVICE=1 (small calls through the resident service, csrc/rle_service.h) and with
 RLE_MI355X_ZC_SEG=0 (no zero-copy segmented form: round 4's first form of the small calls).
 Prints one JSON object.   usage: python tools/e2e_compare.py [--reps 3]
 """
@@ -123,7 +122,6 @@ def main():
     for name, exe, env in (("server_ref", "server_ref", None),
                            ("server_gpu", "server_gpu", None),
                            ("server_gpu_preinit0", "server_gpu", {"RLE_MI355X_PREINIT": "0"}),
-                           ("server_gpu_service", "server_gpu", {"RLE_MI355X_SERVICE": "1"}),
                            ("server_gpu_zcseg0", "server_gpu", {"RLE_MI355X_ZC_SEG": "0"})):
         path = os.path.join(E.BIN, exe)
         if not os.path.exists(path):

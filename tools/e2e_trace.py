@@ -45,8 +45,7 @@ def summarize(path):
 
 def main():
     exe = os.path.join(E.BIN, "server_gpu")
-    for variant, extra in (("default", {}), ("service", {"RLE_MI355X_SERVICE": "1"}),
-                           ("zcseg0", {"RLE_MI355X_ZC_SEG": "0"})):
+    for variant, extra in (("default", {}), ("zcseg0", {"RLE_MI355X_ZC_SEG": "0"})):
         for name in ("battery1", "battery2", "battery3"):
             run(exe, variant, extra, name)
 

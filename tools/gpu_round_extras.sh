@@ -15,12 +15,10 @@ E2E_TRACE_KEEP=$O/traces timeout -k 10 300 python -u $R/tools/e2e_trace.py > $O/
 rc=$?; echo "e2e_trace rc=$rc" >> $O/status_extras; fatal $rc
 bash $R/tools/gpu_sq_kinds.sh ${TAG}_sq k64_zero k64_random k64_runs50 k64_runs90 cfg1
 rc=$?; echo "sq rc=$rc" >> $O/status_extras; fatal $rc
-for S in 0 1; do
-  for T in 1 8 16; do
-    echo "service=$S U=4096 threads=$T" >> $O/callrate.txt
-    RLE_MI355X_SERVICE=$S timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
-    rc=$?; echo "callrate service=$S $T rc=$rc" >> $O/status_extras; fatal $rc
-  done
+for T in 1 8 16; do
+  echo "U=4096 threads=$T" >> $O/callrate.txt
+  timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
+  rc=$?; echo "callrate $T rc=$rc" >> $O/status_extras; fatal $rc
 done
 timeout -k 10 500 python -u $R/tools/e2e_compare.py --reps 2 > $O/e2e_compare.json 2> $O/e2e_compare.err
 rc=$?; echo "e2e_compare rc=$rc" >> $O/status_extras; fatal $rc
