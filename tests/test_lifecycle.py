@@ -19,7 +19,6 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "c-filestorage-server-and-client_amd")
-LC = os.path.join(PKG, "build", "lifecycle")
 DRIVER = os.path.join(REPO, "tests", "native", "lifecycle_driver.c")
 
 pytestmark = pytest.mark.skipif(shutil.which("gcc") is None or shutil.which("g++") is None, reason="needs gcc/g++")
@@ -59,8 +58,9 @@ def test_linked_program_starts_up_in_background(tmp_path):
 
 @pytest.fixture(scope="module")
 def lifecycle_builds(tmp_path_factory):
-    subprocess.run(["make", "-s", "-C", PKG, "lifecycle"], check=True, capture_output=True, timeout=900)
     d = tmp_path_factory.mktemp("lc")
+    LC = str(d)   # (the sanitizer builds stay out of the tree: nothing on the GPU box needs them)
+    subprocess.run(["make", "-s", "-C", PKG, "lifecycle", "LCDIR=" + LC], check=True, capture_output=True, timeout=900)
     exes = {}
     for san, flag in (("asan", "address"), ("tsan", "thread")):
         lib = f"rle_mi355x_lc_{san}"
