@@ -342,6 +342,50 @@ __device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
     }
     return false;
 }
+// A deeper form of walk_tiles (decode tiles only, no lookahead load): kDepth slots, tile t in slot
+// t % kDepth, tile t + kDepth loaded into it by step t's next().  Vector-memory ops complete in
+// issue order, so the wait for tile t (loaded in step t - kDepth, before that step's stores) also
+// waits for every store issued before it: with two slots a step's stores must be acknowledged two
+// steps later, which output-heavy tiles (a 1008-byte tile of zero-filled data stores 3 KB in a few
+// hundred cycles) reach before the stores' latency has passed.  More slots give them more steps.
+// The ops issued after tile t's load: stores(t - D) and, for each step j in (t - D, t), the load of
+// tile j + D (when it exists) and stores(j) (steps j < 0 are the priming loads, without stores).
+template <u32 kDepth>
+__device__ __forceinline__ void walk_ring_prime(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots) {
+    const u32 lo = start + 16u * lane;
+    const u32 l0 = uniform(lds_addr(slots));
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
+#pragma unroll
+    for (u32 d = 0; d < kDepth; ++d)
+        if (d < ntiles) Refill{rs, d * kTileStep + lo, l0 + d * kSlot, true, false}();
+}
+template <u32 kDepth, class Step>
+__device__ __forceinline__ bool walk_ring(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots, Step step) {
+    static_assert(kDepth >= 2u && kDepth <= 6u, "ring depth");
+    const u32 lo = start + 16u * lane;
+    const u32 l0 = uniform(lds_addr(slots));
+    u32 ps[kDepth];   // ps[k]: stores of step t - 1 - k
+#pragma unroll
+    for (u32 k = 0; k < kDepth; ++k) ps[k] = 0u;
+    u32 slot = 0;
+    for (u32 t = 0; t < ntiles; ++t) {
+        u32 nout = ps[kDepth - 1u];   // stores(t - D)
+#pragma unroll
+        for (u32 k = 0; k + 1u < kDepth; ++k)   // step j = t - 1 - k: its load of tile j + D, its stores
+            nout += ps[k] + (t - 1u - k + kDepth < ntiles ? 1u : 0u);
+        vm_wait(nout);
+#pragma unroll
+        for (u32 k = kDepth - 1u; k > 0u; --k) ps[k] = ps[k - 1u];
+        const u32 ls = l0 + slot * kSlot;
+        ps[0] = step(t, slots + slot * kSlot, Refill{rs, (t + kDepth) * kTileStep + lo, ls, t + kDepth < ntiles, false});
+        if (ps[0] == ~0u) {
+            vm_drain();
+            return true;
+        }
+        slot = slot + 1u == kDepth ? 0u : slot + 1u;
+    }
+    return false;
+}
 __device__ __forceinline__ u32 ntiles_for(u32 n) { return (n + kTileStep - 1u) / kTileStep; }
 __device__ __forceinline__ u32 enc_ntiles_for(u32 n) { return (n + kEncStep - 1u) / kEncStep; }
 
@@ -1155,7 +1199,7 @@ __device__ __forceinline__ bool walk_pairs(u32x4 rs, u32 start, u32 ntiles, u32 
 
 // ================================================================ DECODE
 #ifndef RLE_ABL   // ablation builds (timing only, wrong output): 1 no phase scan, 2 no scatter, 4 no fill, 8 scatter without its LDS writes
-#define RLE_ABL 0
+#define RLE_ABL 0     // (16: no count-digit validation -- still exact on encoder output; 32: no uniform-tile test)
 #endif
 // Token-phase table, indexed by an 8-bit mask n of "byte j differs from byte j+1" (the complement
 // of the 3-byte-token mask) and entry offset d (the first token start in the group, 0..2):
@@ -1223,6 +1267,8 @@ struct DecState {
     bool wt;       // write-through output stores (vstore)
     Stamps sp;     // diagnostic builds only
     u32 lit_skip = 0;   // tiles left before the literal path is tried again (RLE_DEC_LITSKIP)
+    u32 vrun = 0;       // RLE_DEC_VRUN: 0x100 | v while the staged partial chunk is all v and staging
+                        // chunk 1 holds exactly one key, kv at position 0 (after a single-value tile)
 };
 
 // Bank spread of the decode staging (RLE_SWZ).  Unswizzled, a random-data tile decodes 16 positions
@@ -1517,7 +1563,7 @@ __device__ __forceinline__ DecLen dec_lengths_t(const DecPrep& p, u32 d) {
         const u32 a = faddi<0x46464646u>(xm);   // bit 7: digit >= ':'
         const u32 b2 = faddi<0x4E4E4E4Eu>(xm);  // bit 7: digit >= '2'
         const u32 b = faddi<0x4F4F4F4Fu>(xm);   // low 7 bits: digit - '1'
-        bad = bitop3<kAndOr>(bitop3<kBad>(a, b2, dg[k]), P80, bad);
+        if (!(RLE_ABL & 16)) bad = bitop3<kAndOr>(bitop3<kBad>(a, b2, dg[k]), P80, bad);
         const u32 S01 = fshr<7>(S80[k]);
         r.S80[k] = S80[k];
         r.S01[k] = S01;
@@ -1764,22 +1810,31 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
 
 // Single-value tile (dec_tile): ttot copies of v after the staged partial chunk.  The caller sets
 // the tile's exit state (st.d, st.prev).
+#ifndef RLE_DEC_VRUN   // 1: consecutive single-value tiles of one byte skip the staging (st.vrun)
+#define RLE_DEC_VRUN 1
+#endif
 __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st) {
     const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl = total >> 4;
     const u32 vv = rep4(v);
-    // chunk 0: the staged positions [0, rel0) filled like a flush, then v (every lane computes it)
-    u32x4 a, b;
-    dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), a, b);
-    u32 L[8];
-    dec_fill_scan(a, b, L);
-    const u32x4 f = dec_fill_out(L, st.fillc);
-    const u32 fv[4] = {f.x, f.y, f.z, f.w};
-    u32 c0[4];
+    // the previous tile was single-value tile of the same byte that left staging chunk 1 as one key
+    // kv at position 0: the staged positions are all v, so chunk 0 is rep4(v) without reading or
+    // filling the staging, and the staging stays as it is when this tile leaves a partial chunk too
+    const bool known = RLE_DEC_VRUN && st.vrun == (0x100u | v);
+    u32 c0[4] = {vv, vv, vv, vv};
+    if (!known) {
+        // chunk 0: the staged positions [0, rel0) filled like a flush, then v (every lane computes it)
+        u32x4 a, b;
+        dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), a, b);
+        u32 L[8];
+        dec_fill_scan(a, b, L);
+        const u32x4 f = dec_fill_out(L, st.fillc);
+        const u32 fv[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-    for (u32 k = 0; k < 4; ++k) {
-        const u32 nb = rel0 > 4u * k ? (rel0 - 4u * k < 4u ? rel0 - 4u * k : 4u) : 0u;
-        const u32 m = lowmask(8u * nb);
-        c0[k] = (fv[k] & m) | (vv & ~m);
+        for (u32 k = 0; k < 4; ++k) {
+            const u32 nb = rel0 > 4u * k ? (rel0 - 4u * k < 4u ? rel0 - 4u * k : 4u) : 0u;
+            const u32 m = lowmask(8u * nb);
+            c0[k] = (fv[k] & m) | (vv & ~m);
+        }
     }
     const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
@@ -1787,20 +1842,23 @@ __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* 
         const u32x4 o = c == 0u ? u32x4{c0[0], c0[1], c0[2], c0[3]} : u32x4{vv, vv, vv, vv};
         vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, o, st.wt);
     }
-    wave_lds_sync();   // every lane has read staging chunk 1
-    // staging chunk 1 = the new partial chunk: the old keys plus a key at rel0 (nothing flushed),
-    // else a key at position 0 (when anything is left) and zeros
-    const u32 kv = kKeyFlag | v;
-    if (lane == 0u) {
-        if (nfl == 0u) {
-            *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(lds_addr(stage) + 32u + 2u * rel0)) = (uint16_t)kv;
-        } else {
-            const u32 k0 = (total & 15u) ? kv : 0u;
-            *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(stage) + 32u)) = u32x4{k0, 0u, 0u, 0u};
-            *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(stage) + 48u)) = u32x4{0u, 0u, 0u, 0u};
+    if (!(known && nfl != 0u && (total & 15u) != 0u)) {
+        wave_lds_sync();   // every lane has read staging chunk 1
+        // staging chunk 1 = the new partial chunk: the old keys plus a key at rel0 (nothing flushed),
+        // else a key at position 0 (when anything is left) and zeros
+        const u32 kv = kKeyFlag | v;
+        if (lane == 0u) {
+            if (nfl == 0u) {
+                *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(lds_addr(stage) + 32u + 2u * rel0)) = (uint16_t)kv;
+            } else {
+                const u32 k0 = (total & 15u) ? kv : 0u;
+                *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(stage) + 32u)) = u32x4{k0, 0u, 0u, 0u};
+                *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(stage) + 48u)) = u32x4{0u, 0u, 0u, 0u};
+            }
         }
+        wave_lds_sync();
     }
-    wave_lds_sync();
+    st.vrun = (nfl != 0u && (total & 15u) != 0u) ? (0x100u | v) : 0u;
     st.fillc = v;
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
@@ -1825,7 +1883,7 @@ __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t*
 // the vector unit, so other tiles pay a few scalar instructions.  Byte-identical to the general
 // path: the same tokens, each 3 bytes long (its first two bytes are equal) with count 9.
 #ifndef RLE_DEC_UNIFORM
-#define RLE_DEC_UNIFORM 1
+#define RLE_DEC_UNIFORM 0   // off since r5: same-process A/B (profiles/r5b_ab.md) cfg1 decode 9.96 -> 9.26 us, 64 KiB runs50 -3 %, random -2 %, zero +0.7 %, dec64k +-0
 #endif
 constexpr u32 kUniformOut = 9u * (kTileStep / 3u);   // 3024
 __device__ __forceinline__ u32 uniform_pat(u32 m, u32 vv) {
@@ -1868,6 +1926,8 @@ __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u3
 #ifndef RLE_DEC_SEGFAST
 #define RLE_DEC_SEGFAST 1
 #endif
+    const u32 vrun = st.vrun;   // (the single-value path below keeps it; every other path changes the staging)
+    st.vrun = 0u;
     const bool head_ok = !st.head || (RLE_DEC_SEGFAST && st.out_pos - st.flushed == st.head);
     // RLE_DEC_LITSKIP > 0: a tile that fails the literal path's test makes the next that many tiles
     // skip it (round-4 experiment): run-heavy data (runs50 / runs90) fails it on every tile, paying
@@ -1915,8 +1975,10 @@ __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u3
             const u32 t = w[k] ^ vv;
             bad |= bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80) & ln.S80[k];
         }
-        if (!(__builtin_amdgcn_ballot_w64(bad != 0u) & kOwned))
+        if (!(__builtin_amdgcn_ballot_w64(bad != 0u) & kOwned)) {
+            st.vrun = vrun;
             return dec_tile_fill(v, ttot, lane, stage, rso, st, pr);
+        }
     }
     RLE_STAMP(st.sp, 1);   // phase maps, token starts, lengths, offsets
     // With the full staging (kDecChunks >= 191) a tile is one pass.  Smaller staging (more waves per
@@ -1977,7 +2039,7 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
-    if (kUni && RLE_DEC_UNIFORM && !st.head && pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
+    if (kUni && RLE_DEC_UNIFORM && !(RLE_ABL & 32) && !st.head && pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
         u32 v;
         if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
             const u32 r = dec_fill_run(v, kUniformOut, lane, stage, rso, st);

@@ -285,6 +285,9 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
 // launcher takes 96 (3 KiB per wave: 7 workgroups per CU instead of 4) for batches past one
 // residency round, where the extra waves hide more latency than the two-pass staging of the
 // output-heavy tiles costs.
+#ifndef RLE_DEC_DEPTH_LARGE   // tile slots per wave of the large-batch decode (walk_ring; 2: walk_tiles)
+#define RLE_DEC_DEPTH_LARGE 2
+#endif
 template <u32 kChunks>
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
@@ -296,7 +299,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt,
                                                            const uint32_t* __restrict__ order) {
     const unsigned long long tl0 = tl_now();
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2 * kSlot];
+    constexpr u32 kDepth = kChunks >= 191u ? 2u : (u32)RLE_DEC_DEPTH_LARGE;
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * kDepth * kSlot];
     constexpr u32 kStageB = 32u * kChunks;
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kStageB];
     __shared__ __attribute__((aligned(16))) DecEntry tbl[256];
@@ -343,7 +347,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         else if (ntiles >= 3u) __builtin_amdgcn_s_setprio(1);
     }
     uint8_t* stage = stage_all + wid * kStageB;
-    const uint8_t* slots = slots_all + wid * 2 * kSlot;
+    const uint8_t* slots = slots_all + wid * kDepth * kSlot;
     // The phase table and the compaction selectors, shared by the workgroup: wave 0 LDS-DMAs them
     // (2.3 KB) after every wave has issued its first tiles' loads, waits for its own table loads
     // (they complete in issue order, its tile loads after them may still be in flight), and one
@@ -351,7 +355,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     // every wave's loads queue at once: one copy per workgroup instead of per wave keeps the
     // table traffic off the first tiles' path.)
     stagger();
-    walk_prime(rsi, 0u, ntiles, lane, slots);
+    if constexpr (kDepth == 2u) walk_prime(rsi, 0u, ntiles, lane, slots);
+    else walk_ring_prime<kDepth>(rsi, 0u, ntiles, lane, slots);
     tl_mark(b, 15, lane);   // (diagnostic builds: the first tiles' loads issued)
     if (wid == 0u) {
         const u32x4 rt = make_rsrc(&kDecTable, (u32)sizeof(DecTable));
@@ -381,13 +386,13 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         st.sp.last = memtime();
 #endif
         tl_mark(b, 1, lane);
-        const bool serial = walk_tiles(
-            rsi, 0u, ntiles, lane, slots,
-            [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                tl_mark(b, 2u + t, lane);
-                return dec_tile<true, kChunks>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
-            },
-            true);
+        auto tile = [&](u32 t, const uint8_t* cs, const Refill& nx) {
+            tl_mark(b, 2u + t, lane);
+            return dec_tile<true, kChunks>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
+        };
+        bool serial;
+        if constexpr (kDepth == 2u) serial = walk_tiles(rsi, 0u, ntiles, lane, slots, tile, true);
+        else serial = walk_ring<kDepth>(rsi, 0u, ntiles, lane, slots, tile);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
         if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage, kStageB);

@@ -218,6 +218,58 @@ def test_single_value_tiles_decode_match_oracle():
             assert dec[i] == ref, (delta, i, len(xs[i]))
 
 
+def test_consecutive_single_value_tiles_decode_match_oracle():
+    """Whole uniform tiles back to back (RLE_DEC_VRUN, csrc/rle_device.h dec_fill_run): runs of
+    3024 k bytes ("v v 9" tokens filling whole 1008-byte tiles) of the same or of different bytes,
+    aligned on tile edges by literal leads of whole tiles, then off the edges, with general and
+    literal tiles between them; 1 and 4500 buffers (both decode kernels), exact / short / overflow U."""
+    rng = np.random.default_rng(31)
+
+    def literals(n):
+        x = rng.integers(0, 255, size=n).astype(np.uint8)
+        for i in range(1, n):   # no two equal neighbours: n literal tokens
+            if x[i] == x[i - 1]:
+                x[i] = (x[i] + 1) % 255
+        return x.tobytes()
+
+    xs = []
+    for lead in (0, 1008, 2016, 1, 17, 1000):
+        for ks in ((1, 1), (2, 3), (1, 1, 1, 1), (3, 1, 2)):
+            for same in (True, False):
+                x = bytearray(literals(lead))
+                v = int(rng.integers(0, 256))
+                for k in ks:
+                    if not same:
+                        v = (v + 1 + int(rng.integers(0, 254))) % 256
+                    x += bytes([v]) * (3024 * k)
+                x += literals(int(rng.integers(0, 3000)))
+                xs.append(bytes(x))
+    for i in range(40):   # uniform tiles, then run-heavy / literal stretches, then uniform again
+        parts = []
+        for _ in range(6):
+            r = rng.random()
+            if r < 0.5:
+                parts.append(bytes([int(rng.integers(0, 256))]) * (3024 * int(rng.integers(1, 4)) + int(rng.integers(0, 3))))
+            elif r < 0.75:
+                parts.append(literals(int(rng.integers(1, 2500))))
+            else:
+                parts.append(O.gen(2, 900 + i, int(rng.integers(1, 4000))))
+        xs.append(b"".join(parts))
+    ys = [O.encode(x) for x in xs]
+    for delta in (0, 7, -5):
+        us = [max(0, len(x) + delta) for x in xs]
+        dec, st = gpu_decode(ys, us)
+        for i, y in enumerate(ys):
+            ref, _ = O.decode(y, us[i])
+            assert dec[i] == ref, (delta, i, len(xs[i]))
+    # the large-batch kernel (96-chunk staging, > 4096 buffers)
+    big = (xs * (4500 // len(xs) + 1))[:4500]
+    ybig = [O.encode(x) for x in big]
+    dec, st = gpu_decode(ybig, [len(x) for x in big])
+    for i, x in enumerate(big):
+        assert dec[i] == x, i
+
+
 def test_large_batch_small_staging_matches_oracle():
     """Batches past one residency round (> 4096 buffers) decode with the 96-chunk staging
     (csrc/rle_kernels.hip decode_kernel<kDecChunksLarge>), where output-heavy general tiles (runs of
