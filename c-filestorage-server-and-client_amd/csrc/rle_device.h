@@ -1029,6 +1029,28 @@ __device__ __forceinline__ bool enc_lit_reject(const EncAn& a, u32 vm) {
     const u32 P = a.B & ~(a.B24 >> 1) & vm;
     return (C18 & (C18 >> 1)) != 0u || __builtin_popcount(P) > 2;
 }
+// Output offsets of a whole literal k64 tile (every position below U) without a DPP scan
+// (RLE_ENC_MBCNT, round 5).  Lane l outputs n_l = 16 - del0_l + p15_l + pc_l (del0: its position 0
+// continues a pair begun before the lane; p15: a pair starts at its position 15; pc <= 2: its pair
+// starts).  With no run longer than 2, p15_l = del0_{l+1}, so the sum over the lanes before l
+// telescopes: exclusive offset 16 l + del0_l - del0_0 + (pairs of the lanes before l, two ballots
+// counted with v_mbcnt); the tile's total from the same ballots, p15_63 from lane 63's lookahead.
+#ifndef RLE_ENC_MBCNT
+#define RLE_ENC_MBCNT 1
+#endif
+__device__ __forceinline__ u32 mbcnt64(uint64_t b) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
+}
+__device__ __forceinline__ void enc_lit_offsets(const EncAn& a, u32 P, u32 lane, u32& ox, u32& tot) {
+    const u32 del0 = (~a.B24) & 1u;
+    const u32 pc = (u32)__builtin_popcount(P);
+    const uint64_t B1 = __builtin_amdgcn_ballot_w64(pc >= 1u), B2 = __builtin_amdgcn_ballot_w64(pc >= 2u);
+    const uint64_t Bd = __builtin_amdgcn_ballot_w64(del0 != 0u);
+    const uint64_t Bp = __builtin_amdgcn_ballot_w64(lane == 63u && ((P >> 15) & 1u) != 0u);
+    const u32 d00 = (u32)Bd & 1u;
+    ox = 16u * lane + del0 - d00 + mbcnt64(B1) + mbcnt64(B2);
+    tot = 16u * kWave + (u32)(Bp >> 63) - d00 + (u32)__builtin_popcountll(B1) + (u32)__builtin_popcountll(B2);
+}
 // first insertion pass (the second, for lanes with two pairs, is the caller's: enc_lit_second)
 __device__ __forceinline__ EncLit enc_lit_first(const EncAn& a, const uint2 look, u32 lane, u32 P, u32 nout,
                                                 const u32* elut) {
@@ -1050,17 +1072,18 @@ __device__ __forceinline__ void enc_lit_second(EncLit& r, const u32* elut) {
     const u32 o1[5] = {r.out[0], r.out[1], r.out[2], r.out[3], r.out[4]};
     enc_lit_insert(elut, o1, r.j2, r.out);
 }
-// the stores of one literal tile whose output starts at base (va: first 16 bytes; vb: last 16)
-__device__ __forceinline__ void enc_lit_store(const EncLit& r, u32 base, u32 oincl, u32x4 rso, bool wt) {
+// the stores of one literal tile whose output starts at base (va: first 16 bytes; vb: last 16);
+// oexcl: the lane's exclusive output offset in the tile
+__device__ __forceinline__ void enc_lit_store(const EncLit& r, u32 base, u32 oexcl, u32x4 rso, bool wt) {
     const u32 n0 = from_next_lane(r.out[0], 0u);
     u32x4 va;
     va.x = r.out[0]; va.y = r.out[1]; va.z = r.out[2];
     va.w = __builtin_amdgcn_perm(n0, r.out[3], r.nout >= 16u ? 0x03020100u : 0x04020100u);
-    const u32 o = base + oincl - r.nout;
+    const u32 o = base + oexcl;
     vstore(rso, r.nout ? o : kOOB, va, wt);
 }
-__device__ __forceinline__ void enc_lit_store_b(const EncLit& r, u32 base, u32 oincl, u32x4 rso, bool wt) {
-    const u32 o = base + oincl - r.nout;
+__device__ __forceinline__ void enc_lit_store_b(const EncLit& r, u32 base, u32 oexcl, u32x4 rso, bool wt) {
+    const u32 o = base + oexcl;
     const u32 b = r.nout - 16u;
     u32x4 vb;
     vb.x = alignbyte(r.out[1], r.out[0], b); vb.y = alignbyte(r.out[2], r.out[1], b);
@@ -1107,8 +1130,18 @@ __device__ __forceinline__ u32 enc_pair(const uint8_t* slotA, const uint8_t* slo
             !((readlane(~a1.B24, 0) & 1u) && rs1 + 1u != pos1)) {
             u32 P0, P1;
             const u32 n0 = enc_lit_count(a0, 0xFFFFu, P0), n1 = enc_lit_count(a1, vm1, P1);
-            const u32 oi0 = wave_scan_incl(n0, 0u, OpAdd()), oi1 = wave_scan_incl(n1, 0u, OpAdd());
-            const u32 t0 = readlane(oi0, 63), t1 = readlane(oi1, 63);
+            u32 oi0, oi1, t0, t1;   // (exclusive offsets, totals)
+            if (RLE_ENC_MBCNT && pos1 + kEncStep <= U) {   // both tiles whole
+                enc_lit_offsets(a0, P0, lane, oi0, t0);
+                enc_lit_offsets(a1, P1, lane, oi1, t1);
+            } else {
+                oi0 = wave_scan_incl(n0, 0u, OpAdd());
+                oi1 = wave_scan_incl(n1, 0u, OpAdd());
+                t0 = readlane(oi0, 63);
+                t1 = readlane(oi1, 63);
+                oi0 -= n0;
+                oi1 -= n1;
+            }
             if (!last1 || t1 >= 4u) {
                 EncLit L0 = enc_lit_first(a0, lookA, lane, P0, n0, elut);
                 EncLit L1 = enc_lit_first(a1, lookB, lane, P1, n1, elut);
@@ -1269,6 +1302,7 @@ struct DecState {
     u32 lit_skip = 0;   // tiles left before the literal path is tried again (RLE_DEC_LITSKIP)
     u32 vrun = 0;       // RLE_DEC_VRUN: 0x100 | v while the staged partial chunk is all v and staging
                         // chunk 1 holds exactly one key, kv at position 0 (after a single-value tile)
+    bool sv = false;    // the last tile was single-value (dec_fill_run): the next tries the uniform test
 };
 
 // Bank spread of the decode staging (RLE_SWZ).  Unswizzled, a random-data tile decodes 16 positions
@@ -1738,8 +1772,28 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     }
     const u32 K = lane < kOwnLanes ? (~del & lim) : ((prevP >> 15) & 1u);
     const u32 kept = (u32)__builtin_popcount(K);
-    const u32 oincl = wave_scan_incl(kept, 0u, OpAdd());
-    const u32 ttot = readlane(oincl, kWave - 1u);
+    // Output offsets.  A whole tile's owned lanes keep 16 - d bytes, d = their deletions (<= 2, else
+    // the tile is rejected below), and lane 63 keeps 0 or 1: so the exclusive offset of lane l is
+    // 16 l less the deletions of the lanes before it, two ballots counted with v_mbcnt, and the
+    // tile's total comes from the same ballots on the scalar unit -- no DPP scan on the tile's
+    // dependent chain (RLE_DEC_MBCNT, round 5).  Tail tiles (owned lanes cut short) take the scan.
+#ifndef RLE_DEC_MBCNT
+#define RLE_DEC_MBCNT 1
+#endif
+    u32 oexcl, ttot;
+    if (RLE_DEC_MBCNT && !kTail) {
+        const u32 d = lane < kOwnLanes ? (u32)__builtin_popcount(del) : 0u;
+        const uint64_t B1 = __builtin_amdgcn_ballot_w64(d >= 1u), B2 = __builtin_amdgcn_ballot_w64(d >= 2u);
+        const uint64_t B3 = __builtin_amdgcn_ballot_w64(lane == kWave - 1u && kept != 0u);
+        const u32 before = __builtin_amdgcn_mbcnt_hi((u32)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((u32)B1, 0u)) +
+                           __builtin_amdgcn_mbcnt_hi((u32)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((u32)B2, 0u));
+        oexcl = 16u * lane - before;
+        ttot = 16u * kOwnLanes - (u32)__builtin_popcountll(B1) - (u32)__builtin_popcountll(B2) + (u32)(B3 >> 63);
+    } else {
+        const u32 oincl = wave_scan_incl(kept, 0u, OpAdd());
+        ttot = readlane(oincl, kWave - 1u);
+        oexcl = oincl - kept;
+    }
     if (__builtin_amdgcn_ballot_w64(reject) & (RLE_DEC_DIGIT2 ? ~0ull : kOwned)) return kNotFast;
     if (kTail ? (ttot < 4u || st.out_pos + ttot > U) : st.out_pos + ttot + 16u > U) return kNotFast;
     if (kTail) {
@@ -1785,7 +1839,7 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     const u32 n0 = from_next_lane(o.x, 0u);
     const u32 s3 = kept >= 16u ? 0x03020100u : kept == 15u ? 0x04020100u : 0x05040100u;
     o.w = lane < kOwnLanes ? __builtin_amdgcn_perm(n0, c3, s3) : c3;
-    vstore(rso, kept ? st.out_pos + oincl - kept : kOOB, o, st.wt);
+    vstore(rso, kept ? st.out_pos + oexcl : kOOB, o, st.wt);
     if (kTail) {
         // the last 4 bytes of each lane's output: from its own bytes, or with fewer than 4 the
         // previous (full) lane's last bytes and its own
@@ -1859,6 +1913,7 @@ __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* 
         wave_lds_sync();
     }
     st.vrun = (nfl != 0u && (total & 15u) != 0u) ? (0x100u | v) : 0u;
+    st.sv = true;
     st.fillc = v;
     st.flushed += 16u * nfl;
     st.out_pos += ttot;
@@ -1882,8 +1937,8 @@ __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t*
 // unit, then every owned byte and the lookahead bytes its last token reads (lane 63's first d) on
 // the vector unit, so other tiles pay a few scalar instructions.  Byte-identical to the general
 // path: the same tokens, each 3 bytes long (its first two bytes are equal) with count 9.
-#ifndef RLE_DEC_UNIFORM
-#define RLE_DEC_UNIFORM 0   // off since r5: same-process A/B (profiles/r5b_ab.md) cfg1 decode 9.96 -> 9.26 us, 64 KiB runs50 -3 %, random -2 %, zero +0.7 %, dec64k +-0
+#ifndef RLE_DEC_UNIFORM   // 0: no uniform-tile test in any kernel (A/B builds)
+#define RLE_DEC_UNIFORM 1
 #endif
 constexpr u32 kUniformOut = 9u * (kTileStep / 3u);   // 3024
 __device__ __forceinline__ u32 uniform_pat(u32 m, u32 vv) {
@@ -1928,6 +1983,7 @@ __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u3
 #endif
     const u32 vrun = st.vrun;   // (the single-value path below keeps it; every other path changes the staging)
     st.vrun = 0u;
+    st.sv = false;   // (dec_fill_run sets it again on the single-value path)
     const bool head_ok = !st.head || (RLE_DEC_SEGFAST && st.out_pos - st.flushed == st.head);
     // RLE_DEC_LITSKIP > 0: a tile that fails the literal path's test makes the next that many tiles
     // skip it (round-4 experiment): run-heavy data (runs50 / runs90) fails it on every tile, paying
@@ -2039,7 +2095,15 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
-    if (kUni && RLE_DEC_UNIFORM && !(RLE_ABL & 32) && !st.head && pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
+    // RLE_DEC_UNIFORM_GATE (round 5): only after a single-value tile (st.sv), so that the test stays
+    // off the dependent chain of every other kind of tile (it cost configs[1] decode 0.56-0.7 us
+    // and the 64 KiB random / run-heavy kinds 2-3 %, profiles/r5b_ab.md, r5c_ab.md), while the long
+    // zero-filled or single-byte stretches it is for take it from their second tile on.
+#ifndef RLE_DEC_UNIFORM_GATE
+#define RLE_DEC_UNIFORM_GATE 1
+#endif
+    if (kUni && RLE_DEC_UNIFORM && !(RLE_ABL & 32) && (st.sv || !RLE_DEC_UNIFORM_GATE) && !st.head &&
+        pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
         u32 v;
         if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
             const u32 r = dec_fill_run(v, kUniformOut, lane, stage, rso, st);

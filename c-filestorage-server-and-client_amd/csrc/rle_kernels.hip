@@ -286,7 +286,18 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
 // residency round, where the extra waves hide more latency than the two-pass staging of the
 // output-heavy tiles costs.
 #ifndef RLE_DEC_DEPTH_LARGE   // tile slots per wave of the large-batch decode (walk_ring; 2: walk_tiles)
-#define RLE_DEC_DEPTH_LARGE 2
+#define RLE_DEC_DEPTH_LARGE 2     // r5c same process: 3 / 4 slots +4-6 % on 64 KiB runs50 / runs90, dec64k +1.2 / +1.7 %
+#endif
+// The uniform-tile test (dec_uniform_tile) per kernel.  r5b / r5c same process (profiles/r5b_ab.md,
+// r5c_ab.md): in the one-round kernel (configs[1]) it cost decode 0.56-0.7 us (10.03 -> 9.47 us),
+// so it is off there; in the large-batch kernel it still pays on the dec64k mix (420.9 against
+// 423.5 us without), although the single-kind 64 KiB batches other than zero are 2-3 % faster
+// without it.
+#ifndef RLE_DEC_UNIFORM_ONE
+#define RLE_DEC_UNIFORM_ONE 1   // (gated by RLE_DEC_UNIFORM_GATE: tried only after a single-value tile)
+#endif
+#ifndef RLE_DEC_UNIFORM_LARGE
+#define RLE_DEC_UNIFORM_LARGE 1
 #endif
 template <u32 kChunks>
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
@@ -388,7 +399,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         tl_mark(b, 1, lane);
         auto tile = [&](u32 t, const uint8_t* cs, const Refill& nx) {
             tl_mark(b, 2u + t, lane);
-            return dec_tile<true, kChunks>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
+            return dec_tile<true, kChunks, (kChunks >= 191u ? RLE_DEC_UNIFORM_ONE : RLE_DEC_UNIFORM_LARGE) != 0>(
+                cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
         };
         bool serial;
         if constexpr (kDepth == 2u) serial = walk_tiles(rsi, 0u, ntiles, lane, slots, tile, true);
