@@ -229,6 +229,23 @@ __device__ __forceinline__ void vm_wait(u32 n) {
     }
 }
 #undef RLE_VMW
+// the same for the deeper walks (walk_ring), whose counts reach past 15
+#define RLE_VMW2(N)                                           \
+    case N:                                                   \
+        asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+        break;
+__device__ __forceinline__ void vm_wait_deep(u32 n) {
+    n = uniform(n);
+    switch (n < 39u ? n : 39u) {
+        RLE_VMW2(0) RLE_VMW2(1) RLE_VMW2(2) RLE_VMW2(3) RLE_VMW2(4) RLE_VMW2(5) RLE_VMW2(6) RLE_VMW2(7)
+        RLE_VMW2(8) RLE_VMW2(9) RLE_VMW2(10) RLE_VMW2(11) RLE_VMW2(12) RLE_VMW2(13) RLE_VMW2(14) RLE_VMW2(15)
+        RLE_VMW2(16) RLE_VMW2(17) RLE_VMW2(18) RLE_VMW2(19) RLE_VMW2(20) RLE_VMW2(21) RLE_VMW2(22) RLE_VMW2(23)
+        RLE_VMW2(24) RLE_VMW2(25) RLE_VMW2(26) RLE_VMW2(27) RLE_VMW2(28) RLE_VMW2(29) RLE_VMW2(30) RLE_VMW2(31)
+        RLE_VMW2(32) RLE_VMW2(33) RLE_VMW2(34) RLE_VMW2(35) RLE_VMW2(36) RLE_VMW2(37) RLE_VMW2(38) RLE_VMW2(39)
+        default: break;
+    }
+}
+#undef RLE_VMW2
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Launch flags, the kernels' `wt` argument: bit 0 write-through output stores (vstore), bit 1 the
@@ -361,7 +378,7 @@ __device__ __forceinline__ void walk_ring_prime(u32x4 rs, u32 start, u32 ntiles,
 }
 template <u32 kDepth, class Step>
 __device__ __forceinline__ bool walk_ring(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots, Step step) {
-    static_assert(kDepth >= 2u && kDepth <= 6u, "ring depth");
+    static_assert(kDepth >= 2u && kDepth <= 8u, "ring depth");
     const u32 lo = start + 16u * lane;
     const u32 l0 = uniform(lds_addr(slots));
     u32 ps[kDepth];   // ps[k]: stores of step t - 1 - k
@@ -373,10 +390,10 @@ __device__ __forceinline__ bool walk_ring(u32x4 rs, u32 start, u32 ntiles, u32 l
 #pragma unroll
         for (u32 k = 0; k + 1u < kDepth; ++k)   // step j = t - 1 - k: its load of tile j + D, its stores
             nout += ps[k] + (t - 1u - k + kDepth < ntiles ? 1u : 0u);
-        vm_wait(nout);
+        vm_wait_deep(nout);
 #pragma unroll
         for (u32 k = kDepth - 1u; k > 0u; --k) ps[k] = ps[k - 1u];
-        const u32 ls = l0 + slot * kSlot;
+        const u32 ls = uniform(l0 + slot * kSlot);
         ps[0] = step(t, slots + slot * kSlot, Refill{rs, (t + kDepth) * kTileStep + lo, ls, t + kDepth < ntiles, false});
         if (ps[0] == ~0u) {
             vm_drain();

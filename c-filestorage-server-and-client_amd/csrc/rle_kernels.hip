@@ -83,6 +83,7 @@ constexpr u32 kEncWaves = RLE_ENC_WAVES;
 #endif
 constexpr u32 kEncSmall = RLE_ENC_SMALL;
 constexpr u32 kEncBlock = kWave * kEncWaves;
+template <u32 kDepth = 2u>
 __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
                                                            const uint64_t* __restrict__ in_len,
@@ -91,13 +92,14 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
                                                            uint64_t* __restrict__ out_len,
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
     const unsigned long long tl0 = tl_now();
-    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * 2 * kEncSlot];
+    constexpr u32 kSlotsB = kDepth > 2u ? kDepth * kSlot : 2u * kEncSlot;   // (ring slots: 1008-byte tiles)
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * kSlotsB];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kEncWaves * kEncStage];
     __shared__ __attribute__((aligned(16))) u32 elut_all[kEncWaves * kInsWaveWords];
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     uint8_t* stage = stage_all + wid * kEncStage;
-    const uint8_t* slots = slots_all + wid * 2 * kEncSlot;
+    const uint8_t* slots = slots_all + wid * kSlotsB;
     const u32 b = xcd_buffer(blockIdx.x, gridDim.x, kEncWaves, wid);
     if (b >= n) return;
     tl_mark(b, 0, lane);
@@ -152,11 +154,18 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
                                            tl_mark(b, 2u + t, lane);
                                            return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
                                        });
-    } else
-        walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+    } else {
+        auto tile = [&](u32 t, const uint8_t* cs, const Refill& nx) {
             tl_mark(b, 2u + t, lane);
             return enc_tile<false, true>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc, elut);
-        });
+        };
+        if constexpr (kDepth > 2u) {
+            walk_ring_prime<kDepth>(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots);
+            walk_ring<kDepth>(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, tile);
+        } else {
+            walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, tile);
+        }
+    }
     RLE_STAMP(st.sp, 6);   // drain
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
     if (lane < st.out_pos - st.flushed) dst[st.flushed + lane] = stage[16u + lane];
@@ -299,7 +308,14 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
 #ifndef RLE_DEC_UNIFORM_LARGE
 #define RLE_DEC_UNIFORM_LARGE 1
 #endif
-template <u32 kChunks>
+// kDepth: tile slots per wave (walk_ring past 2).  Few-buffer launches (kFewBuffers, the drop-in's
+// single calls) take kFewDepth: one wave walking a file over PCIe (zero-copy) or from HBM is bound by
+// the loads in flight, and a launch of a few buffers has LDS to spare.
+#ifndef RLE_FEW_DEPTH
+#define RLE_FEW_DEPTH 8
+#endif
+constexpr u32 kFewDepth = RLE_FEW_DEPTH;
+template <u32 kChunks, u32 kDepthT = 0u>
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
                                                            const uint64_t* __restrict__ in_len,
@@ -310,7 +326,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt,
                                                            const uint32_t* __restrict__ order) {
     const unsigned long long tl0 = tl_now();
-    constexpr u32 kDepth = kChunks >= 191u ? 2u : (u32)RLE_DEC_DEPTH_LARGE;
+    constexpr u32 kDepth = kDepthT ? kDepthT : (kChunks >= 191u ? 2u : (u32)RLE_DEC_DEPTH_LARGE);
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * kDepth * kSlot];
     constexpr u32 kStageB = 32u * kChunks;
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kStageB];
@@ -563,6 +579,7 @@ uint32_t store_policy(uint32_t n, bool enc) {
 // Decode batches past one residency round of the chip (4 workgroups of 4 waves per CU) are
 // issued longest first; RLE_MI355X_DEC_ORDER=0 turns that off.
 constexpr uint32_t kDecRound = 4096;
+constexpr uint32_t kFewBuffers = 16;   // launches of up to this many buffers take the deep tile ring
 #ifndef RLE_DEC_CHUNKS_LARGE   // staging chunks of the decode kernel for batches past kDecRound
 #define RLE_DEC_CHUNKS_LARGE 96
 #endif
@@ -583,7 +600,8 @@ int encode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
-    hipLaunchKernelGGL(rle::encode_kernel, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
+    auto kern = (n <= kFewBuffers && rle::kFewDepth > 2u) ? rle::encode_kernel<rle::kFewDepth> : rle::encode_kernel<2u>;
+    hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n,
                        store_policy(n, true) | flags);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
@@ -619,9 +637,11 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
         hipLaunchKernelGGL(rle::dec_order_hist_kernel, g, dim3(256), 0, s, d_in_len, n, hist);
         hipLaunchKernelGGL(rle::dec_order_scatter_kernel, g, dim3(256), 0, s, d_in_len, n, hist, cursor, order);
     }
-    // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD)
+    // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD);
+    // a few buffers (single drop-in calls): the deep tile ring
     auto kern = n > kDecRound && kDecChunksLarge != rle::kDecChunks ? rle::decode_kernel<kDecChunksLarge>
-                                                                    : rle::decode_kernel<rle::kDecChunks>;
+                : (n <= kFewBuffers && rle::kFewDepth > 2u) ? rle::decode_kernel<rle::kDecChunks, rle::kFewDepth>
+                                                            : rle::decode_kernel<rle::kDecChunks>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
                        d_status, n, store_policy(n, false) | flags, (const uint32_t*)order);
