@@ -309,10 +309,13 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
 #define RLE_DEC_UNIFORM_LARGE 1
 #endif
 // kDepth: tile slots per wave (walk_ring past 2).  Few-buffer launches (kFewBuffers, the drop-in's
-// single calls) take kFewDepth: one wave walking a file over PCIe (zero-copy) or from HBM is bound by
-// the loads in flight, and a launch of a few buffers has LDS to spare.
+// single calls) may take kFewDepth slots (RLE_FEW_DEPTH > 2): one wave walking a file over PCIe
+// (zero-copy) or from HBM with more loads in flight.  Measured (r5e, profiles/r5e_call_latency.md):
+// 8 slots were no faster than 2 at any size from 4 KiB to 128 KiB (random 24 KiB: 36.5 / 36.5 us
+// against 32.3 / 31.9 us per compress / decompress call): a lone wave's walk is bound by its tiles'
+// dependent chains, not by loads in flight.  Off (2).
 #ifndef RLE_FEW_DEPTH
-#define RLE_FEW_DEPTH 8
+#define RLE_FEW_DEPTH 2
 #endif
 constexpr u32 kFewDepth = RLE_FEW_DEPTH;
 template <u32 kChunks, u32 kDepthT = 0u>
@@ -600,7 +603,9 @@ int encode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
-    auto kern = (n <= kFewBuffers && rle::kFewDepth > 2u) ? rle::encode_kernel<rle::kFewDepth> : rle::encode_kernel<2u>;
+    auto kern = rle::encode_kernel<2u>;
+    if constexpr (rle::kFewDepth > 2u)
+        if (n <= kFewBuffers) kern = rle::encode_kernel<rle::kFewDepth>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n,
                        store_policy(n, true) | flags);
@@ -640,8 +645,9 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD);
     // a few buffers (single drop-in calls): the deep tile ring
     auto kern = n > kDecRound && kDecChunksLarge != rle::kDecChunks ? rle::decode_kernel<kDecChunksLarge>
-                : (n <= kFewBuffers && rle::kFewDepth > 2u) ? rle::decode_kernel<rle::kDecChunks, rle::kFewDepth>
-                                                            : rle::decode_kernel<rle::kDecChunks>;
+                                                                    : rle::decode_kernel<rle::kDecChunks>;
+    if constexpr (rle::kFewDepth > 2u)
+        if (n <= kFewBuffers) kern = rle::decode_kernel<rle::kDecChunks, rle::kFewDepth>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
                        d_status, n, store_policy(n, false) | flags, (const uint32_t*)order);

@@ -13,7 +13,7 @@ timeout -k 10 300 python -u -m pytest $R/tests/test_e2e_server.py -m gpu -s -q -
 rc=$?; echo "e2e rc=$rc" >> $O/status_extras; fatal $rc
 E2E_TRACE_KEEP=$O/traces timeout -k 10 300 python -u $R/tools/e2e_trace.py > $O/e2e_trace.json 2> $O/e2e_trace.err
 rc=$?; echo "e2e_trace rc=$rc" >> $O/status_extras; fatal $rc
-bash $R/tools/gpu_sq_kinds.sh ${TAG}_sq k64_zero k64_random k64_runs50 k64_runs90 cfg1
+bash $R/tools/gpu_sq_kinds.sh ${TAG}_sq k64_zero k64_random k64_runs50 k64_runs90 dec64k cfg1
 rc=$?; echo "sq rc=$rc" >> $O/status_extras; fatal $rc
 for T in 1 8 16; do
   echo "U=4096 threads=$T" >> $O/callrate.txt
