@@ -61,7 +61,8 @@ class Server:
         while not os.path.exists(self.sock):
             if self.p.poll() is not None or time.time() - t0 > 60:
                 raise RuntimeError("server did not start: " + self.p.stdout.read().decode(errors="replace"))
-            time.sleep(0.05)
+            time.sleep(0.005)
+        self.startup_s = time.time() - t0   # spawn -> socket (the drop-in's start-up runs before main)
         if settle:
             time.sleep(settle)
 

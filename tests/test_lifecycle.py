@@ -44,7 +44,8 @@ def test_python_load_starts_no_gpu_work():
 
 def test_linked_program_starts_up_in_background(tmp_path):
     """A C program linked against librle_mi355x.so (DT_NEEDED, like the reference server) gets the
-    background start-up by default; RLE_MI355X_PREINIT=0 turns it off."""
+    start-up by default (its main() waits, bounded, for phase 1; without a GPU that ends at once);
+    RLE_MI355X_PREINIT=0 turns it off."""
     src = tmp_path / "pi.c"
     src.write_text("#include <stdio.h>\nint rle_mi355x_preinit_state(void);\n"
                    "int main(void){printf(\"%d\\n\", rle_mi355x_preinit_state());return 0;}\n")
@@ -75,15 +76,19 @@ def lifecycle_builds(tmp_path_factory):
 
 
 @pytest.mark.parametrize("san", ["asan", "tsan"])
-@pytest.mark.parametrize("scenario", ["exit", "workers", "fork", "dlopen"])
+@pytest.mark.parametrize("scenario", ["exit", "exit_nowait", "workers", "fork", "fork_nowait", "dlopen"])
 def test_lifecycle_under_sanitizers(lifecycle_builds, san, scenario):
-    """Immediate exit while the start-up thread builds contexts; exit while worker threads are still
-    in their key destructors; fork during start-up (the child must not wait for a start-up that has
-    no thread in it); dlopen after main with RLE_MI355X_PREINIT=8.  Each must exit 0 with no
-    sanitizer report."""
+    """Immediate exit (after the constructor's wait for phase 1, and with RLE_MI355X_PREINIT_WAIT_MS=0
+    while the start-up thread is still building contexts); exit while worker threads are still in
+    their key destructors; fork during start-up (the child must not wait for a start-up that has no
+    thread in it); dlopen after main with RLE_MI355X_PREINIT=8.  Each must exit 0 with no sanitizer
+    report."""
     exe, exed, lib = lifecycle_builds[san]
     env = {"RLE_MI355X_FAKE_DEVICES": "2", "RLE_MI355X_FAKE_DELAY_US": "5000",
            "ASAN_OPTIONS": "detect_leaks=0:abort_on_error=0", "TSAN_OPTIONS": "halt_on_error=1"}
+    if scenario.endswith("_nowait"):
+        env["RLE_MI355X_PREINIT_WAIT_MS"] = "0"
+        scenario = scenario[:-len("_nowait")]
     if scenario == "dlopen":
         env["RLE_MI355X_PREINIT"] = "8"
         r = _run([exed, "dlopen", lib], env)

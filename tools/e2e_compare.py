@@ -13,7 +13,9 @@ batteries of tests/test_e2e_server.py plus a concurrent one:
 Batteries 1 and 2 are timed twice: from the moment the server's socket appears (cold: the first
 calls may still wait for the drop-in's background start-up) and on a server that has been up for
 SETTLE seconds (started: a serving process).  Every returned file is checked byte for byte.
-server_gpu also runs with RLE_MI355X_PREINIT=0 (round 3's lazy start-up on the first call) and with
+startup_s: spawn to socket (battery 3's server; the drop-in's start-up phase 1 runs before main()
+since round 5).  server_gpu also runs with RLE_MI355X_PREINIT_WAIT_MS=0 (round 4: the start-up in
+the background only), RLE_MI355X_PREINIT=0 (round 3's lazy start-up on the first call) and with
 RLE_MI355X_ZC_SEG=0 (no zero-copy segmented form: round 4's first form of the small calls).
 Prints one JSON object.   usage: python tools/e2e_compare.py [--reps 3]
 """
@@ -84,6 +86,7 @@ def battery3(exe, tmp, env=None):
         hot = concurrent_round(srv, tmp, main, "main")
     finally:
         srv.stop()
+    battery3.startup_s = srv.startup_s
     got = E._returned(tmp)
     for d, fs in warm + main:
         for p, b in fs.items():
@@ -96,7 +99,7 @@ SETTLE = 1.5
 
 def run(exe, env, reps):
     out = {"battery1_s": [], "battery1_started_s": [], "battery2_s": [], "battery2_started_s": [],
-           "battery3_cold_s": [], "battery3_warm_s": []}
+           "battery3_cold_s": [], "battery3_warm_s": [], "startup_s": []}
     for _ in range(reps):
         for settle, key in ((0.0, ""), (SETTLE, "_started")):
             with tempfile.TemporaryDirectory() as tmp:
@@ -111,6 +114,7 @@ def run(exe, env, reps):
             cold, hot = battery3(exe, tmp, env)
             out["battery3_cold_s"].append(round(cold, 4))
             out["battery3_warm_s"].append(round(hot, 4))
+            out["startup_s"].append(round(battery3.startup_s, 4))
     return out
 
 
@@ -121,6 +125,7 @@ def main():
     res = {}
     for name, exe, env in (("server_ref", "server_ref", None),
                            ("server_gpu", "server_gpu", None),
+                           ("server_gpu_nowait", "server_gpu", {"RLE_MI355X_PREINIT_WAIT_MS": "0"}),
                            ("server_gpu_preinit0", "server_gpu", {"RLE_MI355X_PREINIT": "0"}),
                            ("server_gpu_zcseg0", "server_gpu", {"RLE_MI355X_ZC_SEG": "0"})):
         path = os.path.join(E.BIN, exe)
