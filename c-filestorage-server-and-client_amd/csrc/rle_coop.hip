@@ -30,7 +30,7 @@
 
 namespace rle {
 
-constexpr u32 kCoopMaxWaves = 8;
+constexpr u32 kCoopMaxWaves = 16;
 
 __device__ __forceinline__ u32 coop_wave() { return uniform(threadIdx.x / kWave); }
 
@@ -499,7 +499,9 @@ extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off
     else if (tiles <= 3) RLE_ENC_COOP(3);
     else if (tiles <= 4) RLE_ENC_COOP(4);
     else if (tiles <= 6) RLE_ENC_COOP(6);
-    else RLE_ENC_COOP(8);
+    else if (tiles <= 8) RLE_ENC_COOP(8);
+    else if (tiles <= 12) RLE_ENC_COOP(12);
+    else RLE_ENC_COOP(16);
 #undef RLE_ENC_COOP
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
 }
@@ -509,7 +511,7 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
                                       uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint64_t max_out_len,
                                       uint32_t flags, void* stream) {
     if (max_in_len > (uint64_t)rle::kTileStep * rle::kCoopMaxWaves || max_in_len <= rle::kTileStep ||
-        max_out_len > 16384u)
+        max_out_len > 32768u)
         return 0;
     const uint32_t tiles = (uint32_t)((max_in_len + rle::kTileStep - 1) / rle::kTileStep);
     if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
@@ -522,7 +524,11 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
         hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, \
                            d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt);         \
     } while (0)
-    if (max_out_len <= 4096u) {
+    if (max_out_len > 16384u) {   // (highly compressible buffers of 16-32 KiB)
+        if (tiles <= 4) RLE_DEC_COOP(4, 32768);
+        else if (tiles <= 8) RLE_DEC_COOP(8, 32768);
+        else RLE_DEC_COOP(16, 32768);
+    } else if (max_out_len <= 4096u) {
         if (tiles <= 2) RLE_DEC_COOP(2, 4096);
         else if (tiles <= 3) RLE_DEC_COOP(3, 4096);
         else if (tiles <= 5) RLE_DEC_COOP(5, 4096);
@@ -531,7 +537,9 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
         if (tiles <= 2) RLE_DEC_COOP(2, 16384);
         else if (tiles <= 3) RLE_DEC_COOP(3, 16384);
         else if (tiles <= 5) RLE_DEC_COOP(5, 16384);
-        else RLE_DEC_COOP(8, 16384);
+        else if (tiles <= 8) RLE_DEC_COOP(8, 16384);
+        else if (tiles <= 12) RLE_DEC_COOP(12, 16384);
+        else RLE_DEC_COOP(16, 16384);
     }
 #undef RLE_DEC_COOP
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;

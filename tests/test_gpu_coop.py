@@ -56,14 +56,36 @@ def test_every_kind_and_small_size(kind):
     coop_parity([O.gen(kind, 7 * kind + i, s) for i, s in enumerate(sizes)])
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_every_kind_nine_to_sixteen_tiles(kind):
+    # 12- and 16-wave workgroups (encode up to 16 KiB; decode up to 16128 stream bytes); streams
+    # longer than that (random 16 KiB) take the workgroup's one-wave fallback under the hint
+    sizes = [8193, 9216, 10000, 11000, 12287, 12288, 12289, 13000, 15000, 16127, 16128, 16129, 16383, 16384]
+    xs = [O.gen(kind, 11 * kind + i, s) for i, s in enumerate(sizes)]
+    coop_parity(xs, dec_hints=(16128, 16384))
+
+
+@pytest.mark.parametrize("kind", [0, 3])
+def test_compressible_sixteen_to_thirtytwo_kib_decode(kind):
+    # decode staging of 32 KiB (4-, 8- and 16-wave workgroups): compressible buffers of 16-32 KiB,
+    # zero runs crossing the staging's 16 KiB half, and exact-length / ragged ends
+    sizes = [16385, 17000, 20000, 24576, 30000, 32767, 32768]
+    xs = [O.gen(kind, 5 * kind + i, s) for i, s in enumerate(sizes)]
+    xs += [b"\0" * 32768, b"\0" * 16000 + b"x" * 300 + b"\0" * 16468, b"ab" * 8000 + b"\0" * 16768]
+    refs = [O.encode(x) for x in xs]
+    mi = max(len(y) for y in refs)
+    assert mi <= 16128, mi
+    coop_parity(xs, enc_hint=16384, dec_hints=(mi, 32768))
+
+
 def test_runs_and_digits_across_tile_edges():
     # runs that end or cross a tile edge (1008 k decode, 1024 k encode) by 1..10 bytes, digit bytes
     xs = []
-    for k in range(1, 8):
+    for k in range(1, 16):
         for edge in (1008 * k, 1024 * k):
             for r in (1, 2, 3, 8, 9, 10, 11, 18, 19):
                 for side in (-1, 0, 1):
-                    n = min(8192, edge + 40)
+                    n = min(16384, edge + 40)
                     x = bytearray(O.gen(1, 97 * edge + r, n))
                     lo = max(0, edge - r if side <= 0 else edge)
                     hi = min(n, edge + r if side >= 0 else edge)
@@ -71,10 +93,10 @@ def test_runs_and_digits_across_tile_edges():
                     xs.append(bytes(x))
     rng = np.random.default_rng(17)
     for i in range(400):
-        s = int(rng.integers(900, 8192))
+        s = int(rng.integers(900, 16384))
         alpha = np.frombuffer(rng.choice([b"a0123456789", b"\0\x01", b"33", b"ab", b"99"]), np.uint8)
         xs.append(np.repeat(rng.choice(alpha, size=s), rng.integers(1, 22, size=s))[:s].tobytes())
-    coop_parity(xs)
+    coop_parity(xs, dec_hints=(16128, 16384))
 
 
 def test_golden_vectors(vectors):
