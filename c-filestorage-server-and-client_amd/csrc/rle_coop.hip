@@ -20,6 +20,7 @@
 // bytes.  A buffer with more tiles than the workgroup has waves (or, decode, more decoded bytes
 // than its staging) is walked by wave 0 alone with the one-wave tile loop; streams the tiled path
 // declines take the exact serial decoder, as there.
+#include "rle_coop_limits.h"
 #include "rle_device.h"
 #include "rle_service.h"
 
@@ -30,7 +31,8 @@
 
 namespace rle {
 
-constexpr u32 kCoopMaxWaves = 16;
+static_assert(kCoopMaxWaves * kEncStep * kCoopEncRounds == kCoopEncMaxBytes &&
+              kCoopMaxWaves * kTileStep * kCoopDecRounds == kCoopDecMaxIn, "rle_coop_limits.h");
 
 __device__ __forceinline__ u32 coop_wave() { return uniform(threadIdx.x / kWave); }
 
@@ -46,15 +48,18 @@ __device__ __forceinline__ void coop_release(u32 flags) {
 }
 
 // ================================================================ ENCODE
-// kW waves; 1024-byte tiles (enc_tile<true> form), so buffers of up to 1024 kW bytes are coop.
+// kW waves; 1024-byte tiles (enc_tile<true> form), so buffers of up to 1024 kW kR bytes are coop:
+// kR rounds of kW tiles, round r + 1's tiles loading (into the slots round r has read) while round
+// r writes its staging; the run start and output offset entering a round are carried from the last.
 // One buffer (b: its index in out_len / status).  kU (the resident small-call service,
 // rle_service.hip, whose workgroup serves one buffer after another): no wave ends before the last
 // barrier -- the waves without a tile idle through the barriers -- and all of them share the stores.
-template <u32 kW, bool kU>
+template <u32 kW, bool kU, u32 kR = 1>
 __device__ __forceinline__ void enc_coop_body(const uint8_t* src, uint8_t* dst, uint64_t U64,
                                               uint64_t* __restrict__ out_len, uint32_t* __restrict__ status, u32 b,
                                               u32 wt) {
-    constexpr u32 kUmax = kEncStep * kW;
+    static_assert(kR == 1u || !kU, "the service serves one round");
+    constexpr u32 kUmax = kEncStep * kW * kR;
     // output position r at byte 16 + r (chunk 0: guard of the non-starts' back-writes); +32: the
     // writes of positions past U land at the output end
     constexpr u32 kStageC = 16u + kUmax + kUmax / 2u + 32u;
@@ -78,7 +83,7 @@ __device__ __forceinline__ void enc_coop_body(const uint8_t* src, uint8_t* dst, 
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
     const EncK kc = enc_k();
     const u32 ntiles = enc_ntiles_for(U);
-    if (ntiles > kW) {   // too long for one round: wave 0 walks it like encode_kernel
+    if (ntiles > kW * kR) {   // too long for the rounds: wave 0 walks it like encode_kernel
         if (wid != 0u) return;
         EncState st{0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
         if (U <= 16384u)   // rle_kernels.hip kEncSmall
@@ -96,74 +101,88 @@ __device__ __forceinline__ void enc_coop_body(const uint8_t* src, uint8_t* dst, 
         }
         return;
     }
-    const u32 nact = ntiles ? ntiles : 1u;   // waves with a tile (wave 0 also for U = 0)
-    if (!kU && wid >= nact) return;          // ended waves do not hold up s_barrier
+    // waves with a tile in the first round (wave 0 also for U = 0)
+    const u32 nact = ntiles == 0u ? 1u : (ntiles < kW ? ntiles : kW);
+    if (!kU && wid >= nact) return;   // ended waves do not hold up s_barrier
+    const u32 nrounds = kR == 1u || ntiles == 0u ? 1u : (ntiles + kW - 1u) / kW;
     const uint8_t* slot = slots + wid * kEncSlot;
-    const bool act = wid < ntiles;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
-    if (act) Refill{rsi, kEncStep * wid + 16u * lane, uniform(lds_addr(slot)), true, lane == 0u}();
-    vm_drain();
-    __syncthreads();   // every tile has landed
-    EncAn an{};
-    if (act) {
-        const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
-        const uint2 look = *reinterpret_cast<const uint2*>(slot + kSlot);
-        // the input byte before the tile: the previous tile's last byte
-        const u32 prev_top = wid ? *reinterpret_cast<const u32*>(slot - kEncSlot + kSlot - 4u) & 0xFF000000u : 0u;
-        an = enc_analyze_bounds<true>(cur, look, kEncStep * wid, U, U, lane, prev_top, kc);
-        const u32 ilast = readlane(an.incl, kWave - 1u);   // last run boundary in the tile (0: none)
-        if (lane == 0) xch[wid] = ilast;
-    }
-    __syncthreads();
-    u32 nout = 0u, oincl = 0u;
-    if (act) {
-        u32 rs = 0u;   // start of the run holding the byte before the tile
-        for (u32 s = 0; s < wid; ++s) rs = xch[s] > rs ? xch[s] : rs;
-        enc_tokens(an, rs);
-        nout = bcnt(an.P, bcnt(an.P, bcnt(an.T, 0u)));
-        oincl = wave_scan_incl(nout, 0u, OpAdd());
-        if (lane == 0) xch[kW + wid] = readlane(oincl, kWave - 1u);
-    }
-    __syncthreads();
-    u32 O = 0u, total = 0u;
-    for (u32 s = 0; s < ntiles; ++s) {
-        const u32 c = xch[kW + s];
-        O += s < wid ? c : 0u;
-        total += c;
-    }
-    if (act) {
-        const u32* w = an.w;
-        const u32 T = an.T, P = an.P, B24 = an.B24, validm = an.validm;
-        const u32 NS = validm & ~T;
-        const u32 e0 = lds_addr(stage) + 16u + O + oincl - nout;
-        if (kEncStep * wid + kEncStep <= U) enc_pass1<true>(w, T, P, NS, e0, kc.V01);
-        else enc_pass1<false>(w, T, P, NS, e0, 0u);
-        // pass 2 (enc_tile): count digits, and second bytes whose position is the buffer's end
-        const u32 obase = 16u + O + oincl - nout;
-        u32 prem = P;
-        while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
-            if (prem) {
-                const u32 j = (u32)__builtin_ctz(prem);
-                prem &= prem - 1u;
-                const u32 mj = lowmask(j);
-                const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
-                stage[oj + 2u] = (uint8_t)('1' + (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u));
+    if (wid < ntiles) Refill{rsi, kEncStep * wid + 16u * lane, uniform(lds_addr(slot)), true, lane == 0u}();
+    u32 rs_c = 0u, O_c = 0u, top_c = 0u;   // carried into the round: run start, output offset, last byte
+    for (u32 r = 0; r < nrounds; ++r) {
+        const u32 t = r * kW + wid;
+        const bool act = t < ntiles;
+        const u32 rtiles = ntiles - r * kW < kW ? ntiles - r * kW : kW;   // tiles of this round
+        vm_drain();
+        __syncthreads();   // the round's tiles have landed (and the last round's staging is written)
+        EncAn an{};
+        if (act) {
+            const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
+            const uint2 look = *reinterpret_cast<const uint2*>(slot + kSlot);
+            // the input byte before the tile: the previous tile's last byte
+            const u32 prev_top = wid ? *reinterpret_cast<const u32*>(slot - kEncSlot + kSlot - 4u) & 0xFF000000u : top_c;
+            an = enc_analyze_bounds<true>(cur, look, kEncStep * t, U, U, lane, prev_top, kc);
+            const u32 ilast = readlane(an.incl, kWave - 1u);   // last run boundary in the tile (0: none)
+            if (lane == 0) xch[wid] = ilast;
+        }
+        if (kR > 1u && r + 1u < nrounds)   // (the round is full: slot kW - 1 holds its last tile)
+            top_c = *reinterpret_cast<const u32*>(slots + (kW - 1u) * kEncSlot + kSlot - 4u) & 0xFF000000u;
+        __syncthreads();   // every slot read: the next round's tiles may land
+        if (kR > 1u && t + kW < ntiles) Refill{rsi, kEncStep * (t + kW) + 16u * lane, uniform(lds_addr(slot)), true, lane == 0u}();
+        u32 nout = 0u, oincl = 0u;
+        if (act) {
+            u32 rs = rs_c;   // start of the run holding the byte before the tile
+            for (u32 s = 0; s < wid; ++s) rs = xch[s] > rs ? xch[s] : rs;
+            enc_tokens(an, rs);
+            nout = bcnt(an.P, bcnt(an.P, bcnt(an.T, 0u)));
+            oincl = wave_scan_incl(nout, 0u, OpAdd());
+            if (lane == 0) xch[kW + wid] = readlane(oincl, kWave - 1u);
+        }
+        __syncthreads();
+        u32 O = O_c, rtot = 0u, rmax = rs_c;
+        for (u32 s = 0; s < rtiles; ++s) {
+            const u32 c = xch[kW + s];
+            O += s < wid ? c : 0u;
+            rtot += c;
+            rmax = xch[s] > rmax ? xch[s] : rmax;
+        }
+        if (act) {
+            const u32* w = an.w;
+            const u32 T = an.T, P = an.P, B24 = an.B24, validm = an.validm;
+            const u32 NS = validm & ~T;
+            const u32 e0 = lds_addr(stage) + 16u + O + oincl - nout;
+            if (kEncStep * t + kEncStep <= U) enc_pass1<true>(w, T, P, NS, e0, kc.V01);
+            else enc_pass1<false>(w, T, P, NS, e0, 0u);
+            // pass 2 (enc_tile): count digits, and second bytes whose position is the buffer's end
+            const u32 obase = 16u + O + oincl - nout;
+            u32 prem = P;
+            while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
+                if (prem) {
+                    const u32 j = (u32)__builtin_ctz(prem);
+                    prem &= prem - 1u;
+                    const u32 mj = lowmask(j);
+                    const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+                    stage[oj + 2u] = (uint8_t)('1' + (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u));
+                }
+            }
+            const u32 vnext = (validm >> 1) | ((from_next_lane(validm, 0u) & 1u) << 15);
+            const u32 PX = P & ~vnext;
+            if (__builtin_amdgcn_ballot_w64(PX != 0u)) {
+                if (PX) {
+                    const u32 j = (u32)__builtin_ctz(PX);
+                    const u32 mj = lowmask(j);
+                    const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+                    const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
+                    stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
+                }
             }
         }
-        const u32 vnext = (validm >> 1) | ((from_next_lane(validm, 0u) & 1u) << 15);
-        const u32 PX = P & ~vnext;
-        if (__builtin_amdgcn_ballot_w64(PX != 0u)) {
-            if (PX) {
-                const u32 j = (u32)__builtin_ctz(PX);
-                const u32 mj = lowmask(j);
-                const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
-                const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
-                stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
-            }
-        }
+        O_c += rtot;
+        rs_c = rmax;
     }
     __syncthreads();
     // store: whole 16-byte chunks, then the final partial chunk byte by byte (nothing past C)
+    const u32 total = O_c;
     const u32 nthr = kWave * (kU ? kW : nact), t = threadIdx.x, nfull = total >> 4;
     for (u32 c = t; c < nfull; c += nthr)
         vstore(rso, 16u * c, *reinterpret_cast<const u32x4*>(stage + 16u + 16u * c), (wt & kLaunchWt) != 0u);
@@ -174,7 +193,7 @@ __device__ __forceinline__ void enc_coop_body(const uint8_t* src, uint8_t* dst, 
         put_status(status, b, RLE_STATUS_OK, wt);
     }
 }
-template <u32 kW>
+template <u32 kW, u32 kR = 1>
 __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __restrict__ in,
                                                              const uint64_t* __restrict__ in_off,
                                                              const uint64_t* __restrict__ in_len,
@@ -184,25 +203,33 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
                                                              uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
     const u32 b = blockIdx.x;
     if (b >= n) return;
-    enc_coop_body<kW, false>(in + in_off[b], out + out_off[b], in_len[b], out_len, status, b, wt);
+    enc_coop_body<kW, false, kR>(in + in_off[b], out + out_off[b], in_len[b], out_len, status, b, wt);
 }
 
 // ================================================================ DECODE
-// kW waves (tiles of 1008 bytes: dec_tile's geometry); buffers decoding to at most kUmax bytes.
+// kW waves (tiles of 1008 bytes: dec_tile's geometry); buffers decoding to at most kUmax bytes from
+// at most kR kW tiles: kR rounds of kW tiles as in enc_coop_body, the token phase and output offset
+// carried across rounds, every round scattering into the one staging; then the fill and the stores.
 // One buffer (b: its index in status; kU as enc_coop_body).
-template <u32 kW, u32 kUmax, bool kU>
+template <u32 kW, u32 kUmax, bool kU, u32 kR = 1>
 __device__ __forceinline__ void dec_coop_body(const uint8_t* src, uint8_t* dst, uint64_t C64, uint64_t U64,
                                               uint64_t cap, uint32_t* __restrict__ status, u32 b, u32 wt) {
     // decoded position r at u16 16 + r (dec_tile's staging, one for the whole buffer); the one-wave
     // fallback needs kDecStage
     constexpr u32 kStageC = 2u * (16u + kUmax + 32u);
     constexpr u32 kStage = ((kStageC > kDecStage ? kStageC : kDecStage) + 127u) & ~127u;
+    static_assert(kR == 1u || !kU, "the service serves one round");
     constexpr u32 kChunks = (kUmax + 15u) / 16u;
-    __shared__ __attribute__((aligned(16))) uint8_t slots[(kW > 2u ? kW : 2u) * kSlot];
+    constexpr u32 kSlotsB = (kW > 2u ? kW : 2u) * kSlot;
+    // the fill's chunk-to-chunk bytes: in the slots (free by then) when they fit, which keeps the
+    // 64 KiB staging within the CU's LDS
+    constexpr bool kLastInSlots = 4u * kChunks <= kSlotsB && kUmax > 32768u;
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kSlotsB];
     __shared__ __attribute__((aligned(128))) uint8_t stage[kStage];
     __shared__ DecEntry tbl[256];
     __shared__ u32 xch[4 * kW];   // per tile: phase map, decoded length, serial, tail byte
-    __shared__ u32 lastb[kChunks + 1];
+    __shared__ u32 lastb_own[kLastInSlots ? 1u : kChunks + 1u];
+    u32* const lastb = kLastInSlots ? reinterpret_cast<u32*>(slots) : lastb_own;
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = coop_wave();
     for (u32 i = threadIdx.x; i < 256u; i += kWave * kW) tbl[i] = dec_entry_from(kDecTable.e[i]);
@@ -218,7 +245,7 @@ __device__ __forceinline__ void dec_coop_body(const uint8_t* src, uint8_t* dst, 
     const u32 ntiles = ntiles_for(C);
     const DecK kc = dec_k();
     __syncthreads();   // the phase table is complete
-    if (ntiles > kW || U > kUmax) {   // wave 0 walks it like decode_kernel
+    if (ntiles > kW * kR || U > kUmax) {   // wave 0 walks it like decode_kernel
         if (wid != 0u) return;
         walk_prime(rsi, 0u, ntiles, lane, slots);
         for (u32 k = lane; k < kDecStage / 16u; k += kWave) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
@@ -237,67 +264,80 @@ __device__ __forceinline__ void dec_coop_body(const uint8_t* src, uint8_t* dst, 
         if (lane == 0) put_status(status, b, stat, wt);
         return;
     }
-    const u32 nact = ntiles ? ntiles : 1u;
+    // waves with a tile in the first round (wave 0 also for C = 0)
+    const u32 nact = ntiles == 0u ? 1u : (ntiles < kW ? ntiles : kW);
     if (!kU && wid >= nact) return;   // ended waves do not hold up s_barrier
     const u32 nthr = kWave * (kU ? kW : nact);   // threads zeroing, filling and storing
+    const u32 nrounds = kR == 1u || ntiles == 0u ? 1u : (ntiles + kW - 1u) / kW;
     const uint8_t* slot = slots + wid * kSlot;
-    const bool act = wid < ntiles;
     asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
-    if (act) dma_tile(rsi, kTileStep * wid + 16u * lane, uniform(lds_addr(slot)));
+    if (wid < ntiles) dma_tile(rsi, kTileStep * wid + 16u * lane, uniform(lds_addr(slot)));
     // the staging positions this buffer can reach: [0, 16 + U + 17) u16
     const u32 nz = (2u * (16u + U + 17u) + 15u) / 16u;
     for (u32 k = threadIdx.x; k < nz; k += nthr) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
-    vm_drain();
-    __syncthreads();   // tiles landed; table and zeroed staging visible
-    DecPrep pr{};
-    if (act) {
-        const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
-        pr = dec_prepare(cur, kTileStep * wid, C, C, lane, tbl, kc);
-        if (lane == 0) xch[wid] = readlane(pr.incl, kOwnLanes - 1u);   // the tile's phase map
-    }
-    __syncthreads();
-    DecLen ln{};
-    u32 oincl = 0u;
-    if (act) {
-        u32 d = 0u;   // token phase entering the tile
-        for (u32 s = 0; s < wid; ++s) d = bfe(xch[s], 8u * d, 8);
-        ln = dec_lengths(pr, d);
-        oincl = wave_scan_incl(ln.nout, 0u, OpAdd());
-        constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
-        const bool serial = (__builtin_amdgcn_ballot_w64(ln.serial_lane) & kOwned) != 0ull;
-        u32 tailv = 0u;
-        if (pr.tail) {
-            const uint64_t pfb = __builtin_amdgcn_ballot_w64(ln.PF != 0u) & kOwned;
-            if (pfb) {   // the final token's byte extends to U
-                const u32 jf = (u32)__builtin_ctz(ln.PF | 0x10000u) & 15u;
-                const u32* w = pr.w;
-                const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
-                tailv = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+    u32 d_c = 0u, O_c = 0u, tail = 0u;   // carried into the round: token phase, output offset, tail byte
+    for (u32 r = 0; r < nrounds; ++r) {
+        const u32 t = r * kW + wid;
+        const bool act = t < ntiles;
+        const u32 rtiles = ntiles - r * kW < kW ? ntiles - r * kW : kW;   // tiles of this round
+        vm_drain();
+        __syncthreads();   // tiles landed; table and zeroed staging visible; the last round scattered
+        DecPrep pr{};
+        if (act) {
+            const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
+            pr = dec_prepare(cur, kTileStep * t, C, C, lane, tbl, kc);
+            if (lane == 0) xch[wid] = readlane(pr.incl, kOwnLanes - 1u);   // the tile's phase map
+        }
+        __syncthreads();   // every slot read: the next round's tiles may land
+        if (kR > 1u && t + kW < ntiles) dma_tile(rsi, kTileStep * (t + kW) + 16u * lane, uniform(lds_addr(slot)));
+        DecLen ln{};
+        u32 oincl = 0u;
+        if (act) {
+            u32 d = d_c;   // token phase entering the tile
+            for (u32 s = 0; s < wid; ++s) d = bfe(xch[s], 8u * d, 8);
+            ln = dec_lengths(pr, d);
+            oincl = wave_scan_incl(ln.nout, 0u, OpAdd());
+            constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+            const bool serial = (__builtin_amdgcn_ballot_w64(ln.serial_lane) & kOwned) != 0ull;
+            u32 tailv = 0u;
+            if (pr.tail) {
+                const uint64_t pfb = __builtin_amdgcn_ballot_w64(ln.PF != 0u) & kOwned;
+                if (pfb) {   // the final token's byte extends to U
+                    const u32 jf = (u32)__builtin_ctz(ln.PF | 0x10000u) & 15u;
+                    const u32* w = pr.w;
+                    const u32 wf = jf < 4u ? w[0] : jf < 8u ? w[1] : jf < 12u ? w[2] : w[3];
+                    tailv = 0x100u | readlane(bfe(wf, 8u * (jf & 3u), 8), (u32)__builtin_ctzll(pfb));
+                }
+            }
+            if (lane == 0) {
+                xch[kW + wid] = readlane(oincl, kOwnLanes - 1u);
+                xch[2 * kW + wid] = serial ? 1u : 0u;
+                xch[3 * kW + wid] = tailv;
             }
         }
-        if (lane == 0) {
-            xch[kW + wid] = readlane(oincl, kOwnLanes - 1u);
-            xch[2 * kW + wid] = serial ? 1u : 0u;
-            xch[3 * kW + wid] = tailv;
+        __syncthreads();
+        u32 O = O_c, rtot = 0u, serial = 0u, d_next = d_c;
+        for (u32 s = 0; s < rtiles; ++s) {
+            const u32 c = xch[kW + s];
+            O += s < wid ? c : 0u;
+            rtot += c;
+            serial |= xch[2 * kW + s];
+            tail |= xch[3 * kW + s];
+            d_next = bfe(xch[s], 8u * d_next, 8);
         }
-    }
-    __syncthreads();
-    u32 O = 0u, total = 0u, serial = 0u, tail = 0u;
-    for (u32 s = 0; s < ntiles; ++s) {
-        const u32 c = xch[kW + s];
-        O += s < wid ? c : 0u;
-        total += c;
-        serial |= xch[2 * kW + s];
-        tail |= xch[3 * kW + s];
-    }
-    if (serial || total > U) {   // not encoder output: the exact serial decoder (dec_tile declines)
-        if (wid == 0u) {
-            const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage);
-            if (lane == 0) put_status(status, b, stat, wt);
+        if (serial || O_c + rtot > U) {   // not encoder output: the exact serial decoder (dec_tile declines)
+            vm_drain();   // (the next round's tiles: nothing lands in the LDS after the workgroup)
+            if (wid == 0u) {
+                const u32 stat = dec_serial(src, C, U, cap, dst, lane, stage);
+                if (lane == 0) put_status(status, b, stat, wt);
+            }
+            return;
         }
-        return;
+        if (act && lane < kOwnLanes && !(RLE_ABL & 2)) dec_scatter(ln, pr.w, lds_addr(stage) + 2u * (16u + O + oincl - ln.nout));
+        O_c += rtot;
+        d_c = d_next;
     }
-    if (act && lane < kOwnLanes && !(RLE_ABL & 2)) dec_scatter(ln, pr.w, lds_addr(stage) + 2u * (16u + O + oincl - ln.nout));
+    const u32 total = O_c;
     __syncthreads();
     // output chunk q (bytes [16q, 16q + 16)) = staging chunk q + 1: decoded positions below total,
     // then the tail byte (zero unless the stream ends in an unbounded token); every chunk holds a
@@ -332,7 +372,7 @@ __device__ __forceinline__ void dec_coop_body(const uint8_t* src, uint8_t* dst, 
     coop_release(wt);
     if (threadIdx.x == 0) put_status(status, b, total < U ? RLE_STATUS_SHORT : RLE_STATUS_OK, wt);
 }
-template <u32 kW, u32 kUmax>
+template <u32 kW, u32 kUmax, u32 kR = 1>
 __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __restrict__ in,
                                                              const uint64_t* __restrict__ in_off,
                                                              const uint64_t* __restrict__ in_len,
@@ -344,7 +384,7 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     const u32 b = blockIdx.x;
     if (b >= n) return;
     const uint64_t* capp = out_cap ? out_cap : out_len;
-    dec_coop_body<kW, kUmax, false>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
+    dec_coop_body<kW, kUmax, false, kR>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
 }
 
 #ifndef RLE_VARIANTS
@@ -483,25 +523,27 @@ bool coop_admits(uint32_t threads, uint32_t n) {
 extern "C" int rle_encode_coop_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
                                       const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
                                       uint64_t max_len, uint32_t flags, void* stream) {
-    if (max_len > rle::kEncStep * rle::kCoopMaxWaves || max_len <= rle::kEncStep) return 0;
+    if (max_len > rle::kEncStep * rle::kCoopMaxWaves * rle::kCoopEncRounds || max_len <= rle::kEncStep) return 0;
     const uint32_t tiles = (uint32_t)((max_len + rle::kEncStep - 1) / rle::kEncStep);
     if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
     const hipStream_t s = (hipStream_t)stream;
     const uint32_t wt = coop_store_policy(n) | flags;
     const dim3 g(n);
-#define RLE_ENC_COOP(W)                                                                                         \
+#define RLE_ENC_COOP(W, R)                                                                                      \
     do {                                                                                                        \
-        if (!coop_admits<rle::enc_coop_kernel<W>>(64 * W, n)) return 0;                             \
-        hipLaunchKernelGGL(rle::enc_coop_kernel<W>, g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off,     \
+        if (!coop_admits<rle::enc_coop_kernel<W, R>>(64 * W, n)) return 0;                                      \
+        hipLaunchKernelGGL((rle::enc_coop_kernel<W, R>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, \
                            d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt);                   \
     } while (0)
-    if (tiles <= 2) RLE_ENC_COOP(2);
-    else if (tiles <= 3) RLE_ENC_COOP(3);
-    else if (tiles <= 4) RLE_ENC_COOP(4);
-    else if (tiles <= 6) RLE_ENC_COOP(6);
-    else if (tiles <= 8) RLE_ENC_COOP(8);
-    else if (tiles <= 12) RLE_ENC_COOP(12);
-    else RLE_ENC_COOP(16);
+    if (tiles <= 2) RLE_ENC_COOP(2, 1);
+    else if (tiles <= 3) RLE_ENC_COOP(3, 1);
+    else if (tiles <= 4) RLE_ENC_COOP(4, 1);
+    else if (tiles <= 6) RLE_ENC_COOP(6, 1);
+    else if (tiles <= 8) RLE_ENC_COOP(8, 1);
+    else if (tiles <= 12) RLE_ENC_COOP(12, 1);
+    else if (tiles <= 16) RLE_ENC_COOP(16, 1);
+    else if (tiles <= 32) RLE_ENC_COOP(16, 2);
+    else RLE_ENC_COOP(16, 4);
 #undef RLE_ENC_COOP
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
 }
@@ -510,24 +552,30 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
                                       const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap,
                                       uint32_t* d_status, uint32_t n, uint64_t max_in_len, uint64_t max_out_len,
                                       uint32_t flags, void* stream) {
-    if (max_in_len > (uint64_t)rle::kTileStep * rle::kCoopMaxWaves || max_in_len <= rle::kTileStep ||
-        max_out_len > 32768u)
+    if (max_in_len > (uint64_t)rle::kTileStep * rle::kCoopMaxWaves * rle::kCoopDecRounds ||
+        max_in_len <= rle::kTileStep || max_out_len > rle::kCoopDecUmax)
         return 0;
     const uint32_t tiles = (uint32_t)((max_in_len + rle::kTileStep - 1) / rle::kTileStep);
     if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
     const hipStream_t s = (hipStream_t)stream;
     const uint32_t wt = coop_store_policy(n) | flags;
     const dim3 g(n);
-#define RLE_DEC_COOP(W, UM)                                                                                      \
-    do {                                                                                                         \
-        if (!coop_admits<rle::dec_coop_kernel<W, UM>>(64 * W, n)) return 0;                          \
-        hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, \
-                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt);         \
+#define RLE_DEC_COOP_R(W, UM, R)                                                                                    \
+    do {                                                                                                            \
+        if (!coop_admits<rle::dec_coop_kernel<W, UM, R>>(64 * W, n)) return 0;                                      \
+        hipLaunchKernelGGL((rle::dec_coop_kernel<W, UM, R>), g, dim3(64 * W), 0, s, (const uint8_t*)d_in, d_in_off, \
+                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap, d_status, n, wt);            \
     } while (0)
-    if (max_out_len > 16384u) {   // (highly compressible buffers of 16-32 KiB)
+#define RLE_DEC_COOP(W, UM) RLE_DEC_COOP_R(W, UM, 1)
+    if (max_out_len > 32768u) {   // 32-64 KiB: rounds of 16 tiles
+        RLE_DEC_COOP_R(16, 65536, 5);
+    } else if (max_out_len > 16384u) {
         if (tiles <= 4) RLE_DEC_COOP(4, 32768);
         else if (tiles <= 8) RLE_DEC_COOP(8, 32768);
-        else RLE_DEC_COOP(16, 32768);
+        else if (tiles <= 16) RLE_DEC_COOP(16, 32768);
+        else RLE_DEC_COOP_R(16, 32768, 3);
+    } else if (tiles > 16) {   // (random 16 KiB: 17 tiles)
+        RLE_DEC_COOP_R(16, 16384, 2);
     } else if (max_out_len <= 4096u) {
         if (tiles <= 2) RLE_DEC_COOP(2, 4096);
         else if (tiles <= 3) RLE_DEC_COOP(3, 4096);
@@ -542,6 +590,7 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
         else RLE_DEC_COOP(16, 16384);
     }
 #undef RLE_DEC_COOP
+#undef RLE_DEC_COOP_R
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
 }
 

@@ -39,6 +39,7 @@
 #include "rle_fileops.h"
 #include "rle_mi355x.h"
 #include "rle_service.h"
+#include "rle_coop_limits.h"
 
 // Measured-slower host-path variants (call coalescing, pipelined staging) are compiled only into the
 // test library (build/librle_mi355x_testhooks.so) and `make variant` builds, never into the product
@@ -156,6 +157,10 @@ bool g_service = false;
 // threads: 40 KB 42.2 / 91.7 against 66.1 / 151.3 for one wave over the mapped buffer; 24 KiB
 // 41.2 / 91.1 against 34.8 / 64.2 (the five launches cost more than a short walk).
 size_t g_zc_seg = 32u << 10;
+// ... except the calls one cooperative workgroup takes (rle_coop_limits.h: encode up to 64 KiB,
+// decode up to 80 tiles decoding to 64 KiB; rounds of 16 waves, one launch, polled like the smaller
+// calls).  RLE_MI355X_ZC_COOP=0: the segmented kernels from g_zc_seg as before (round 5 A/B).
+bool g_zc_coop = true;
 constexpr size_t kZcIn = 0, kZcWords = 64u << 10, kZcOut = 68u << 10, kZcBytes = 256u << 10;
 constexpr size_t kZcMaxIn = kZcWords, kZcMaxOut = kZcBytes - kZcOut;   // one zero-copy call's bytes
 
@@ -284,6 +289,7 @@ void init_once() {
     if (const char* e = getenv("RLE_MI355X_POLL")) g_poll = strcmp(e, "0") != 0;
     if (const char* e = getenv("RLE_MI355X_SERVICE")) g_service = strcmp(e, "0") != 0;
     if (const char* e = getenv("RLE_MI355X_ZC_SEG")) g_zc_seg = (size_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("RLE_MI355X_ZC_COOP")) g_zc_coop = strcmp(e, "0") != 0;
 #if RLE_VARIANTS
     if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
 #endif
@@ -1130,7 +1136,7 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
         C = r.result;
     } else
 #endif
-    if (g_zc_seg && U >= g_zc_seg) {   // several waves over the mapped buffer (segmented kernels)
+    if (g_zc_seg && U >= g_zc_seg && !(g_zc_coop && U <= rle::kCoopEncMaxBytes)) {   // segmented kernels
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = 0;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
@@ -1175,7 +1181,7 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
         st = (uint32_t)r.result;
     } else
 #endif
-    if (g_zc_seg && C >= g_zc_seg) {   // several waves over the mapped buffer (segmented kernels)
+    if (g_zc_seg && C >= g_zc_seg && !(g_zc_coop && C <= rle::kCoopDecMaxIn && U <= rle::kCoopDecUmax)) {   // segmented
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);

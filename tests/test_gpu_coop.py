@@ -67,15 +67,53 @@ def test_every_kind_nine_to_sixteen_tiles(kind):
 
 @pytest.mark.parametrize("kind", [0, 3])
 def test_compressible_sixteen_to_thirtytwo_kib_decode(kind):
-    # decode staging of 32 KiB (4-, 8- and 16-wave workgroups): compressible buffers of 16-32 KiB,
-    # zero runs crossing the staging's 16 KiB half, and exact-length / ragged ends
+    # decode staging of 32 KiB (4-, 8- and 16-wave workgroups, one round): compressible buffers of
+    # 16-32 KiB, zero runs crossing the staging's 16 KiB half, and exact-length / ragged ends; then
+    # with a literal-heavy buffer in the batch (22 tiles: three rounds)
     sizes = [16385, 17000, 20000, 24576, 30000, 32767, 32768]
     xs = [O.gen(kind, 5 * kind + i, s) for i, s in enumerate(sizes)]
-    xs += [b"\0" * 32768, b"\0" * 16000 + b"x" * 300 + b"\0" * 16468, b"ab" * 8000 + b"\0" * 16768]
-    refs = [O.encode(x) for x in xs]
-    mi = max(len(y) for y in refs)
+    xs += [b"\0" * 32768, b"\0" * 16000 + b"x" * 300 + b"\0" * 16468]
+    mi = max(len(O.encode(x)) for x in xs)
     assert mi <= 16128, mi
     coop_parity(xs, enc_hint=16384, dec_hints=(mi, 32768))
+    xs.append(b"ab" * 8000 + b"\0" * 16768)
+    coop_parity(xs, dec_hints=(max(len(O.encode(x)) for x in xs), 32768))
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("umax", [16384, 32768, 65536])
+def test_rounds_of_sixteen_tiles(kind, umax):
+    """Rounds of 16 waves (rle_coop_limits.h): encode 17-64 tiles (2 and 4 rounds), decode 17-80
+    tiles into 16 / 32 / 64 KiB staging; sizes at the round edges (16 x 1024 encode, 16 x 1008
+    decode), with the batch's own hints and with the largest hints of the staging (buffers past the
+    rounds: the workgroup's one-wave fallback)."""
+    sizes = [1500, 8000, 16000, 16128, 16129, 16384, 16385, 20000, 24576, 32256, 32257, 32767, 32768, 40000,
+             48384, 48385, 50000, 64512, 65535, 65536]
+    xs = [O.gen(kind, 13 * kind + i, s) for i, s in enumerate(s for s in sizes if s <= umax)]
+    coop_parity(xs)
+    coop_parity(xs, dec_hints=(1008 * 16 * (2 if umax == 16384 else 3 if umax == 32768 else 5), umax))
+
+
+def test_rounds_invalid_streams_take_serial_decoder():
+    # a stream the tiled path declines only in a later round (a bad digit past 16 tiles), a stream
+    # that decodes past U in a later round, and a valid one in the same batch
+    x = O.gen(3, 5, 60000)
+    y = bytearray(O.encode(x))
+    z = bytearray(y)
+    k = len(z) - 40
+    while not (0x31 <= z[k] <= 0x39 and z[k - 1] == z[k - 2]):
+        k -= 1
+    z[k] = ord(":")   # a count byte past '9': not encoder output
+    streams = [bytes(y), bytes(z), bytes(y) + b"ab" * 100]
+    us = [len(x), len(x), len(x)]
+    caps = [len(x), len(x) + 32, len(x) + 32]
+    dec, st = gpu_decode(streams, us, caps, poison=False, max_in_len=max(len(s) for s in streams),
+                         max_out_len=max(us))
+    for i, (s, u, c) in enumerate(zip(streams, us, caps)):
+        ref, rst = O.decode(s, u, c)
+        assert dec[i] == ref, i
+    import rle_mi355x as R
+    assert st[0] == 0 and st[2] & R.RLE_STATUS_SERIAL and st[2] & R.RLE_STATUS_OVERFLOW, st
 
 
 def test_runs_and_digits_across_tile_edges():
