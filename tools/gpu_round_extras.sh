@@ -20,6 +20,13 @@ for T in 1 8 16; do
   timeout -k 10 60 $R/tools/callrate $T 4096 2 >> $O/callrate.txt 2>&1
   rc=$?; echo "callrate $T rc=$rc" >> $O/status_extras; fatal $rc
 done
+for T in 1 8; do
+  echo "U=32768 threads=$T" >> $O/callrate.txt
+  timeout -k 10 60 $R/tools/callrate $T 32768 2 >> $O/callrate.txt 2>&1
+  rc=$?; echo "callrate32k $T rc=$rc" >> $O/status_extras; fatal $rc
+done
+timeout -k 10 200 python -u $R/tools/call_latency_probe.py 0.3 > $O/call_latency.json 2> $O/call_latency.err
+rc=$?; echo "call_latency rc=$rc" >> $O/status_extras; fatal $rc
 timeout -k 10 500 python -u $R/tools/e2e_compare.py --reps 3 > $O/e2e_compare.json 2> $O/e2e_compare.err
 rc=$?; echo "e2e_compare rc=$rc" >> $O/status_extras; fatal $rc
 bash $R/tools/gpu_sq2.sh ${TAG}_sq2 k64_runs50 k64_zero cfg1
