@@ -287,9 +287,10 @@ def copy_ceiling(B, alg, reps, stream):
             "op": "the faster of rle_copy_device (16 B per lane, hand-written) and hipMemcpyAsync, device to device"}
 
 
-def step_kernels(B, reps, stream, loop_gpu_s=None, steps=None):
+def step_kernels(B, reps, stream, loop_gpu_s=None, steps=None, loop_src="timed_loop_events"):
     """Per-kernel durations consistent with the timed steps.  The GPU time of the timed loop itself
-    (HIP events on the launch stream around the K timed steps, loop_gpu_s) is split between the two
+    (HIP events on the launch stream around the K timed steps, or around the same K steps run again
+    right after the timed region, loop_gpu_s; loop_src says which) is split between the two
     kernels in the ratio of their back-to-back single-kernel times, so encode + decode is the timed
     step's GPU time and never exceeds ms_per_step (round 3 split a separate back-to-back pair run
     after the timed loop, which on the driver box came out 9 % above the step).  Without the loop's
@@ -299,7 +300,7 @@ def step_kernels(B, reps, stream, loop_gpu_s=None, steps=None):
     t_pair = time_kernels(lambda: (B.encode(stream), B.decode(stream)), reps, stream)
     f = t_enc1 / (t_enc1 + t_dec1)
     t_step = loop_gpu_s / steps if loop_gpu_s and steps else t_pair
-    return t_step * f, t_step * (1 - f), {"split_of": "timed_loop_events" if loop_gpu_s and steps else "pair_us",
+    return t_step * f, t_step * (1 - f), {"split_of": loop_src if loop_gpu_s and steps else "pair_us",
                                           "timed_loop_gpu_us_per_step": t_step * 1e6, "pair_us": t_pair * 1e6,
                                           "encode_alone_us": t_enc1 * 1e6, "decode_alone_us": t_dec1 * 1e6}
 
@@ -570,7 +571,12 @@ def run_rank(args):
     # HIP events on the launch stream bracket the same K steps (GPU time of the timed loop): the
     # per-kernel durations are this time split by the kernels' ratio (measure_kernels), so they sum to
     # at most ms_per_step
-    ev = None if dry else (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    # No HIP events inside the timed region (default): the loop's GPU time comes from the same K steps
+    # run again right after it, untimed, between two events.  r5i (profiles/r5i_timed_events.md): the
+    # two event records cost ~0.3 us per step at the driver's 20 steps (graph 772-778 against 779-784
+    # GiB/s).  RLE_BENCH_TIMED_EVENTS=1: the events bracket the timed steps themselves (round 4).
+    timed_ev = os.environ.get("RLE_BENCH_TIMED_EVENTS", "0") != "0"
+    ev = None if (dry or not timed_ev) else (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
     if ev:
         ev[0].record(stream)
@@ -582,6 +588,15 @@ def run_rank(args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     loop_gpu_s = ev[0].elapsed_time(ev[1]) * 1e-3 if ev else None
+    if not dry and not timed_ev:
+        loop.steps(max(1, args.warmup))
+        sync(dry)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        loop.steps(args.steps)
+        e1.record(stream)
+        sync(dry)
+        loop_gpu_s = e0.elapsed_time(e1) * 1e-3
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -613,7 +628,8 @@ def run_rank(args):
 
     kern = roofline = conc = north = cpu = None
     if not dry:
-        kern, roofline = measure_kernels(B, args, stream, u_local, c_bytes, loop_gpu_s)
+        kern, roofline = measure_kernels(B, args, stream, u_local, c_bytes, loop_gpu_s,
+                                         "timed_loop_events" if timed_ev else "rerun_events")
         if rank == 0 and not multi:
             conc = concurrent_streams(B, wl, args, stream, dev)
             if not args.no_north_star and args.workload != "dec64k":
@@ -642,6 +658,7 @@ def run_rank(args):
                "verified_bit_exact_roundtrip": ok, "host_wait": sched,
                "issue": ("one HIP graph of the K timed steps (captured before the timed region), replayed"
                          if loop.plain else "eager: 2 launches per step from the host"),
+               "timed_region_events": timed_ev,
                "value_eager": eager["value"] if eager else None,
                "ms_per_step_eager": eager["ms_per_step"] if eager else None,
                "kernels": kern, "roofline": roofline,
@@ -659,11 +676,11 @@ def run_rank(args):
         dist.destroy_process_group()
 
 
-def measure_kernels(B, args, stream, u_local, c_bytes, loop_gpu_s=None):
+def measure_kernels(B, args, stream, u_local, c_bytes, loop_gpu_s=None, loop_src="timed_loop_events"):
     """Per-kernel durations (HIP events on the launch stream; step_kernels), algorithmic bytes =
     U + C per launch, and the roofline object of the dominant kernel."""
     reps = max(10, min(args.steps, 50))
-    t_enc, t_dec, detail = step_kernels(B, reps, stream, loop_gpu_s, args.steps)
+    t_enc, t_dec, detail = step_kernels(B, reps, stream, loop_gpu_s, args.steps, loop_src)
     alg = u_local + c_bytes
     # GBps: algorithmic bytes (U + C) per second, the roofline numerator; U_GiBps: uncompressed bytes
     # per second (SURVEY.md 8(d) reports both), also for the round trip
