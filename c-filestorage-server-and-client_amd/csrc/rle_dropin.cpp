@@ -292,6 +292,7 @@ void init_once() {
     if (const char* e = getenv("RLE_MI355X_SERVICE")) g_service = strcmp(e, "0") != 0;
     if (const char* e = getenv("RLE_MI355X_ZC_SEG")) g_zc_seg = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_ZC_COOP")) g_zc_coop = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RLE_MI355X_COOP")) g_zc_coop = g_zc_coop && strcmp(e, "0") != 0;   // (no workgroups to take them)
 #if RLE_VARIANTS
     if (const char* e = getenv("RLE_MI355X_COALESCE")) g_coalesce = strcmp(e, "0") != 0;
 #endif
