@@ -29,6 +29,10 @@
 
 #include <atomic>
 
+#ifndef RLE_VARIANTS
+#define RLE_VARIANTS 0
+#endif
+
 namespace rle {
 
 static_assert(kCoopMaxWaves * kEncStep * kCoopEncRounds == kCoopEncMaxBytes &&
@@ -205,6 +209,153 @@ __global__ __launch_bounds__(kWave* kW) void enc_coop_kernel(const uint8_t* __re
     if (b >= n) return;
     enc_coop_body<kW, false, kR>(in + in_off[b], out + out_off[b], in_len[b], out_len, status, b, wt);
 }
+
+// ---------------------------------------------------------------- encode, any size, one pass
+// (round 5, measured no faster than the segmented encode on 1 MiB buffers and slower on zero-filled
+// ones, DESIGN.md §4: in the RLE_VARIANTS test library only)
+#if RLE_VARIANTS
+// One workgroup of kW waves walks a whole buffer in rounds of kW tiles (enc_coop_body's rounds),
+// reading each input byte once: a round's output is staged, its whole 16-byte chunks stored, and
+// the partial chunk carried to the staging's front for the next round.  The staging holds one
+// round's output (at most 1.5 x 1024 kW bytes) past the carried chunk, so any buffer size fits.
+// Thread 0 stores chunk 0 and then moves the partial chunk onto it (no other thread reads chunk 0
+// or writes the partial chunk in that phase), so a round has four barriers.
+template <u32 kW>
+__device__ __forceinline__ void enc_stream_body(const uint8_t* src, uint8_t* dst, uint64_t U64,
+                                                uint64_t* __restrict__ out_len, uint32_t* __restrict__ status, u32 b,
+                                                u32 wt) {
+    constexpr u32 kRoundOut = kEncStep * kW + kEncStep * kW / 2u;
+    constexpr u32 kStage = (16u + 16u + kRoundOut + 32u + 127u) & ~127u;
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kW * kEncSlot];
+    __shared__ __attribute__((aligned(128))) uint8_t stage[kStage];
+    __shared__ u32 xch[2 * kW];
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = coop_wave();
+    u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
+    if (U64 > kMaxBufferBytes) bad |= RLE_STATUS_TOOLARGE;
+    if (bad) {
+        if (threadIdx.x == 0) {
+            out_len[b] = 0;
+            put_status(status, b, bad, wt);
+        }
+        return;
+    }
+    const u32 U = (u32)U64;
+    const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U + U / 2u);
+    const EncK kc = enc_k();
+    const bool wtb = (wt & kLaunchWt) != 0u;
+    const u32 ntiles = enc_ntiles_for(U);
+    const u32 nact = ntiles == 0u ? 1u : (ntiles < kW ? ntiles : kW);
+    if (wid >= nact) return;   // ended waves do not hold up s_barrier
+    const u32 nthr = kWave * nact;
+    const u32 nrounds = ntiles == 0u ? 1u : (ntiles + kW - 1u) / kW;
+    const uint8_t* slot = slots + wid * kEncSlot;
+    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh (walk_prime)
+    if (wid < ntiles) Refill{rsi, kEncStep * wid + 16u * lane, uniform(lds_addr(slot)), true, lane == 0u}();
+    // carried: run start, output offset, last input byte; base = output offset of staging byte 16
+    u32 rs_c = 0u, O_c = 0u, top_c = 0u, base = 0u;
+    u32 nst = 0u;   // store instructions this wave issued after the round's tile loads (the last round)
+    for (u32 r = 0; r < nrounds; ++r) {
+        const u32 t = r * kW + wid;
+        const bool act = t < ntiles;
+        const u32 rtiles = ntiles - r * kW < kW ? ntiles - r * kW : kW;
+        vm_wait_deep(nst);   // the tile loads, not the stores issued after them (vmcnt is in order)
+        __syncthreads();   // the round's tiles have landed; the carried chunk is in place
+        EncAn an{};
+        if (act) {
+            const u32x4 cur = *reinterpret_cast<const u32x4*>(slot + 16u * lane);
+            const uint2 look = *reinterpret_cast<const uint2*>(slot + kSlot);
+            const u32 prev_top = wid ? *reinterpret_cast<const u32*>(slot - kEncSlot + kSlot - 4u) & 0xFF000000u : top_c;
+            an = enc_analyze_bounds<true>(cur, look, kEncStep * t, U, U, lane, prev_top, kc);
+            if (lane == 0) xch[wid] = readlane(an.incl, kWave - 1u);
+        }
+        if (r + 1u < nrounds)
+            top_c = *reinterpret_cast<const u32*>(slots + (kW - 1u) * kEncSlot + kSlot - 4u) & 0xFF000000u;
+        __syncthreads();   // every slot read: the next round's tiles may land
+        if (t + kW < ntiles) Refill{rsi, kEncStep * (t + kW) + 16u * lane, uniform(lds_addr(slot)), true, lane == 0u}();
+        u32 nout = 0u, oincl = 0u;
+        if (act) {
+            u32 rs = rs_c;
+            for (u32 s = 0; s < wid; ++s) rs = xch[s] > rs ? xch[s] : rs;
+            enc_tokens(an, rs);
+            nout = bcnt(an.P, bcnt(an.P, bcnt(an.T, 0u)));
+            oincl = wave_scan_incl(nout, 0u, OpAdd());
+            if (lane == 0) xch[kW + wid] = readlane(oincl, kWave - 1u);
+        }
+        __syncthreads();
+        u32 O = O_c, rtot = 0u, rmax = rs_c;
+        for (u32 s = 0; s < rtiles; ++s) {
+            const u32 c = xch[kW + s];
+            O += s < wid ? c : 0u;
+            rtot += c;
+            rmax = xch[s] > rmax ? xch[s] : rmax;
+        }
+        if (act) {
+            const u32* w = an.w;
+            const u32 T = an.T, P = an.P, B24 = an.B24, validm = an.validm;
+            const u32 NS = validm & ~T;
+            const u32 obase = 16u + (O - base) + oincl - nout;
+            const u32 e0 = lds_addr(stage) + obase;
+            if (kEncStep * t + kEncStep <= U) enc_pass1<true>(w, T, P, NS, e0, kc.V01);
+            else enc_pass1<false>(w, T, P, NS, e0, 0u);
+            u32 prem = P;
+            while (__builtin_amdgcn_ballot_w64(prem != 0u)) {
+                if (prem) {
+                    const u32 j = (u32)__builtin_ctz(prem);
+                    prem &= prem - 1u;
+                    const u32 mj = lowmask(j);
+                    const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+                    stage[oj + 2u] = (uint8_t)('1' + (u32)__builtin_ctz((B24 >> (j + 1u)) | 0x100u));
+                }
+            }
+            const u32 vnext = (validm >> 1) | ((from_next_lane(validm, 0u) & 1u) << 15);
+            const u32 PX = P & ~vnext;
+            if (__builtin_amdgcn_ballot_w64(PX != 0u)) {
+                if (PX) {
+                    const u32 j = (u32)__builtin_ctz(PX);
+                    const u32 mj = lowmask(j);
+                    const u32 oj = bcnt(P & mj, bcnt(P & mj, bcnt(T & mj, obase)));
+                    const u32 wj = j < 4u ? w[0] : j < 8u ? w[1] : j < 12u ? w[2] : w[3];
+                    stage[oj + 1u] = (uint8_t)(wj >> (8u * (j & 3u)));
+                }
+            }
+        }
+        O_c += rtot;
+        rs_c = rmax;
+        __syncthreads();   // the round's output is staged
+        // whole chunks of [base, O_c) out; the partial one to the front (thread 0, after chunk 0)
+        const u32 nfull = (O_c - base) >> 4;
+        for (u32 c = threadIdx.x; c < nfull; c += nthr)
+            vstore(rso, base + 16u * c, *reinterpret_cast<const u32x4*>(stage + 16u + 16u * c), wtb);
+        if (threadIdx.x == 0u && nfull)
+            *reinterpret_cast<u32x4*>(stage + 16u) = *reinterpret_cast<const u32x4*>(stage + 16u + 16u * nfull);
+        base += 16u * nfull;
+        const u32 w0 = kWave * wid;
+        nst = uniform(nfull > w0 ? (nfull - w0 + nthr - 1u) / nthr : 0u);
+    }
+    __syncthreads();
+    const u32 total = O_c;
+    if (threadIdx.x < total - base) dst[base + threadIdx.x] = stage[16u + threadIdx.x];
+    coop_release(wt);
+    if (threadIdx.x == 0) {
+        out_len[b] = total;
+        put_status(status, b, RLE_STATUS_OK, wt);
+    }
+}
+template <u32 kW>
+__global__ __launch_bounds__(kWave* kW) void enc_stream_kernel(const uint8_t* __restrict__ in,
+                                                               const uint64_t* __restrict__ in_off,
+                                                               const uint64_t* __restrict__ in_len,
+                                                               uint8_t* __restrict__ out,
+                                                               const uint64_t* __restrict__ out_off,
+                                                               uint64_t* __restrict__ out_len,
+                                                               uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
+    const u32 b = blockIdx.x;
+    if (b >= n) return;
+    enc_stream_body<kW>(in + in_off[b], out + out_off[b], in_len[b], out_len, status, b, wt);
+}
+#endif  // RLE_VARIANTS (one-pass encode)
 
 // ================================================================ DECODE
 // kW waves (tiles of 1008 bytes: dec_tile's geometry); buffers decoding to at most kUmax bytes from
@@ -387,9 +538,6 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     dec_coop_body<kW, kUmax, false, kR>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
 }
 
-#ifndef RLE_VARIANTS
-#define RLE_VARIANTS 0
-#endif
 #if RLE_VARIANTS   // the resident service is built into the test library only (round 5)
 // ================================================================ resident small-call service
 // (rle_service.h): one workgroup per drop-in thread context.  Wave 0 polls the context's mailbox
@@ -593,6 +741,42 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
 #undef RLE_DEC_COOP_R
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
 }
+
+#if RLE_VARIANTS
+namespace {
+std::atomic<int> g_stream_waves{0};   // 0: from RLE_MI355X_STREAM_WAVES at the first launch
+}
+// Tests: waves per workgroup of the one-pass kernels (4, 8 or 16).
+extern "C" int rle_mi355x_set_stream_waves(int w) {
+    if (w != 4 && w != 8 && w != 16) return RLE_E_INVAL;
+    g_stream_waves.store(w, std::memory_order_relaxed);
+    return RLE_OK;
+}
+// One workgroup per buffer over the whole buffer (enc_stream_body), any size: RLE_OK if launched.
+// RLE_MI355X_STREAM_WAVES (8 or 16, default 16): waves per workgroup.
+extern "C" int rle_encode_stream_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                                        const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status, uint32_t n,
+                                        uint32_t flags, void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t wt = coop_store_policy(n) | flags;
+    if (g_stream_waves.load(std::memory_order_relaxed) == 0) {
+        const char* e = getenv("RLE_MI355X_STREAM_WAVES");
+        g_stream_waves.store(e && atoi(e) == 8 ? 8 : 16, std::memory_order_relaxed);
+    }
+    if (g_stream_waves.load(std::memory_order_relaxed) == 4)
+        hipLaunchKernelGGL(rle::enc_stream_kernel<4>, dim3(n), dim3(64 * 4), 0, s, (const uint8_t*)d_in, d_in_off,
+                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt);
+    else if (g_stream_waves.load(std::memory_order_relaxed) == 8)
+        hipLaunchKernelGGL(rle::enc_stream_kernel<8>, dim3(n), dim3(64 * 8), 0, s, (const uint8_t*)d_in, d_in_off,
+                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt);
+    else
+        hipLaunchKernelGGL(rle::enc_stream_kernel<16>, dim3(n), dim3(64 * 16), 0, s, (const uint8_t*)d_in, d_in_off,
+                           d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n, wt);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
+#endif
 
 // Tests: switch the cooperative mode in-process (0 never, 1 always, -1 residency-gated default).
 extern "C" int rle_mi355x_set_coop_mode(int mode) {

@@ -65,6 +65,9 @@ def lib():
     u64 = ctypes.c_uint64
     L.rle_encode_batch_device_sized.restype = ctypes.c_int
     L.rle_encode_batch_device_sized.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u64, vp]
+    if hasattr(L, "rle_encode_stream_launch"):   # the RLE_VARIANTS test library only (round 5)
+        L.rle_encode_stream_launch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]
+        L.rle_mi355x_set_stream_waves.argtypes = [ctypes.c_int]
     L.rle_decode_batch_device_sized.restype = ctypes.c_int
     L.rle_decode_batch_device_sized.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u64, u64, vp]
     L.rle_encode_batch_device_sized_flags.restype = ctypes.c_int
@@ -220,6 +223,22 @@ def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, str
                                                  _ptr(out_len), _ptr(status), n, int(max_len), _stream_ptr(stream))
     if rc != RLE_OK:
         raise RLEError(f"rle_encode_batch_device failed: {rc}")
+
+
+def encode_batch_stream(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None, flags=0):
+    """Batched encode, one workgroup per buffer walking it in rounds of tiles (csrc/rle_coop.hip
+    enc_stream_body): every input byte read once, any buffer size.  Round 5, measured no faster than
+    the segmented encode: in the RLE_VARIANTS test library only (RLE_MI355X_LIB)."""
+    rc = lib().rle_encode_stream_launch(_ptr(d_in), _ptr(in_off), _ptr(in_len), _ptr(d_out), _ptr(out_off),
+                                        _ptr(out_len), _ptr(status), in_off.numel(), int(flags), _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_encode_stream_launch failed: {rc}")
+
+
+def set_stream_waves(w):
+    """Tests: waves per workgroup of the one-pass kernels (4, 8 or 16)."""
+    if lib().rle_mi355x_set_stream_waves(int(w)) != RLE_OK:
+        raise RLEError(f"set_stream_waves({w})")
 
 
 def decode_batch(d_in, in_off, in_len, d_out, out_off, out_len, out_cap=None, status=None, stream=None,

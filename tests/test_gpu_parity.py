@@ -26,10 +26,11 @@ def _i64(vals):
     return torch.tensor(np.asarray(vals, dtype=np.int64), device=DEV)
 
 
-def gpu_encode(bufs, seg=False, max_len=None, flags=0):
+def gpu_encode(bufs, seg=False, max_len=None, flags=0, one_pass=False):
     """Encode a list of byte strings in ONE batched launch (seg: the segmented multi-wave form;
     max_len: the sized entry point with that hint, which picks the cooperative kernels for small
-    buffers); returns (outputs, status)."""
+    buffers; one_pass: a workgroup per buffer in rounds, rle_encode_stream_launch); returns
+    (outputs, status)."""
     n = len(bufs)
     sizes = [len(b) for b in bufs]
     in_offs, in_total = R.layout(sizes)
@@ -41,7 +42,9 @@ def gpu_encode(bufs, seg=False, max_len=None, flags=0):
     d_out = torch.full((out_total + 16,), POISON, dtype=torch.uint8, device=DEV)
     out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
     status = torch.full((n,), 0x7777, dtype=torch.int32, device=DEV)
-    if max_len is not None:
+    if one_pass:
+        R.encode_batch_stream(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status, flags=flags)
+    elif max_len is not None:
         R.encode_batch(d_in, _i64(in_offs), _i64(sizes), d_out, _i64(out_offs), out_len, status, max_len=max_len,
                        flags=flags)
     else:
