@@ -23,7 +23,7 @@ def main():
     L.RLEdecompress.restype = ctypes.c_void_p
     out = []
     for kind in ("random", "runs"):
-        for U in (4096, 8192, 16384, 24576, 32768, 40000, 49152, 65536, 131072):
+        for U in (4096, 8192, 16384, 24576, 32768, 40000, 49152, 65536, 98304, 131072, 262144, 524288, 1048576):
             x = gen(kind, U, U + 1)
             c = ctypes.c_size_t(0)
             p = L.RLEcompress(x, U, ctypes.byref(c))
