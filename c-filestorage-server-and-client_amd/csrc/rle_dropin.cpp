@@ -152,7 +152,7 @@ bool g_poll = true;
 // RLE_MI355X_SERVICE=1, in the RLE_VARIANTS test library only (measured slower, round 5).
 bool g_service = false;
 // Zero-copy calls from this many bytes (encode: U, decode: C) run the segmented kernels on the mapped
-// buffer instead of one wave walking it, and the zero-copy form then takes calls up to 80 KiB in
+// buffer instead of one wave walking it, and the zero-copy form then takes calls up to 256 KiB in
 // (RLE_MI355X_ZC_SEG=<bytes>; 0 = never).  profiles/r4f_callrate_zcseg.txt, µs per call on 1 / 8
 // threads: 40 KB 42.2 / 91.7 against 66.1 / 151.3 for one wave over the mapped buffer; 24 KiB
 // 41.2 / 91.1 against 34.8 / 64.2 (the five launches cost more than a short walk).
@@ -161,8 +161,14 @@ size_t g_zc_seg = 32u << 10;
 // decode up to 80 tiles decoding to 64 KiB; rounds of 16 waves, one launch, polled like the smaller
 // calls).  RLE_MI355X_ZC_COOP=0: the segmented kernels from g_zc_seg as before (round 5 A/B).
 bool g_zc_coop = true;
-// (input up to 80 KiB: a 64 KiB file's stream, up to the cooperative decode's 80 tiles)
-constexpr size_t kZcIn = 0, kZcWords = 80u << 10, kZcOut = 84u << 10, kZcBytes = 272u << 10;
+// Input up to 256 KiB, output up to 384 KiB (r5n / r5o, profiles/r5o_zc_size.md: past the cooperative
+// kernels' reach the segmented kernels on the mapped buffer beat the two copies of the staged path up
+// to 256 KiB, e.g. a 96 KiB compress 43 against 68 us; 80 KiB of input until round 5's r5n)
+#ifndef RLE_ZC_IN_KIB
+#define RLE_ZC_IN_KIB 256
+#endif
+constexpr size_t kZcIn = 0, kZcWords = (size_t)RLE_ZC_IN_KIB << 10, kZcOut = kZcWords + (4u << 10),
+                 kZcBytes = kZcOut + (kZcWords * 3 / 2 > (204u << 10) ? kZcWords * 3 / 2 : (204u << 10));
 static_assert(kZcWords >= rle::kCoopDecMaxIn, "zero-copy input region");
 constexpr size_t kZcMaxIn = kZcWords, kZcMaxOut = kZcBytes - kZcOut;   // one zero-copy call's bytes
 

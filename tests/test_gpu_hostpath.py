@@ -184,6 +184,17 @@ for k in range(40):
     if R.decompress(y, U, E) != x + bytes(E):
         errors.append(("dec-mid", k, U, E))
 
+# 64-400 KiB calls: past the cooperative kernels, the zero-copy segmented form up to its 256 KiB of
+# input (and 384 KiB of output), the copying form past it; sizes at both reaches
+for k, U in enumerate([65537, 80640, 80641, 98304, 131072, 200000, 262143, 262144, 262145, 300000, 409600]):
+    x = O.gen(k % 5, 70000 + k, U)
+    y = O.encode(x)
+    if R.compress(x) != y:
+        errors.append(("enc-big", k, U))
+    E = 393216 - U if k % 2 == 0 and U < 393216 else 0   # the output region's reach, exactly
+    if R.decompress(y, U, E) != x + bytes(E):
+        errors.append(("dec-big", k, U, E))
+
 def work(t):
     try:
         for k in range(150):
