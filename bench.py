@@ -91,6 +91,8 @@ WORKLOADS = {
     "k64_random": dict(n=16384, size=65536, kinds=(1,), ref_kinds="1", desc="16384 x 64 KiB random"),
     "k64_runs50": dict(n=16384, size=65536, kinds=(2,), ref_kinds="2", desc="16384 x 64 KiB runs50"),
     "k64_runs90": dict(n=16384, size=65536, kinds=(3,), ref_kinds="3", desc="16384 x 64 KiB runs90"),
+    # two kinds side by side (profiling: does a store-bound kind overlap a run-heavy one)
+    "k64_z50": dict(n=16384, size=65536, kinds=(0, 2), ref_kinds="0,2", desc="16384 x 64 KiB zero / runs50"),
     # configs[1] shape with one data kind (profiling: per-SIMD balance of the mixed batch)
     "c4k_random": dict(n=4096, size=4096, kinds=(1,), ref_kinds="1", desc="4096 x 4 KiB random"),
     "c4k_zero": dict(n=4096, size=4096, kinds=(0,), ref_kinds="0", desc="4096 x 4 KiB zero"),

@@ -344,8 +344,18 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     // with an issue order, workgroups take its ranks in dispatch order (the heavy buffers first,
     // spread over every XCD); else each XCD takes a contiguous slice of the batch
     u32 b;
-    if (order) {
-        const u32 slot = blockIdx.x * kDecWaves + wid;
+#ifndef RLE_ORDER_MODE   // A/B only: 1 heavy / light workgroup blocks of 8 alternate; 2 heavy / light waves
+#define RLE_ORDER_MODE 0     // alternate inside a workgroup; 3 the order ignored (index order)
+#endif
+    if (order && RLE_ORDER_MODE != 3) {
+        u32 slot = blockIdx.x * kDecWaves + wid;
+        if (RLE_ORDER_MODE == 1 && (gridDim.x & 7u) == 0u) {
+            const u32 nb = gridDim.x >> 3, h = blockIdx.x >> 3;
+            const u32 ph = (h & 1u) ? nb - 1u - (h >> 1) : (h >> 1);
+            slot = (8u * ph + (blockIdx.x & 7u)) * kDecWaves + wid;
+        } else if (RLE_ORDER_MODE == 2 && slot < n) {
+            slot = (slot & 1u) ? n - 1u - (slot >> 1) : (slot >> 1);
+        }
         b = slot < n ? uniform(order[slot]) : n;
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
