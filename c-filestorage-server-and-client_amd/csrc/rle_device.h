@@ -2132,6 +2132,152 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     return dec_tile_pr<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
 }
 
+// ---------------------------------------------------------------- two literal tiles per step
+// The one-round decode kernel (configs[1]: every buffer's wave resident at once, 4-5 tiles of a
+// 4 KiB random buffer walked one after the other) is bound by each wave's chain of dependent tile
+// steps.  Two whole literal tiles (dec_tile_fast's conditions) are independent but for tile B's entry
+// phase (tile A's exit, a readlane of A's phase scan) and its output offset (A's total), so a step
+// takes both: both preparations, both literal analyses and both compactions, with nothing between
+// them that waits on the other, then A's store and B's.  dec_lit_an is dec_tile_fast<false>'s test
+// and offsets, branch-free (the pair decides once for both tiles); dec_lit_emit its compaction and
+// store.  Any other pair (a run, a tail tile, a general tile) is decoded one tile after the other.
+struct DecLit {
+    u32 del, kept, oexcl, ttot;
+    bool reject;
+};
+__device__ __forceinline__ DecLit dec_lit_an(const DecPrep& pr, u32 lane, u32 d) {
+    const u32* w = pr.w;
+    const u32 NE16 = (pr.xa >> 7) | (pr.xb << 1);
+    const u32 dl = bfe(pr.excl, 8u * d, 8);
+    const u32 mid = __builtin_amdgcn_perm(0u, pr.ta.y, 0x0C0C0C00u | dl);
+    const u32 sa = __builtin_amdgcn_perm(0u, pr.ta.x, 0x0C0C0C00u | dl);
+    const u32 sb = __builtin_amdgcn_perm(0u, pr.tb.x, 0x0C0C0C00u | mid);
+    const u32 P16 = (sa | (sb << 8)) & ~NE16 & 0xFFFFu;   // pair starts
+    const u32 prevP = from_prev_lane(P16, 0u);
+    const u32 dig = ((P16 << 2) | (prevP >> 14)) & 0xFFFFu;   // the pairs' count digits
+    DecLit r;
+    r.del = lane == 0u ? dig | lowmask(d) : dig;
+    // every deleted digit is '2' (lane 63: those of lane 62's pairs), at most 2 per owned lane
+    const u32 chk = lane < kOwnLanes ? dig : ((prevP >> 14) & 3u);
+    const u32 c1 = (u32)__builtin_ctz(chk | 0x10000u), c2 = (u32)__builtin_ctz((chk & (chk - 1u)) | 0x10000u);
+    auto byte_at = [&](u32 q) {
+        const u32 lo = __builtin_amdgcn_perm(w[1], w[0], q & 7u), hi = __builtin_amdgcn_perm(w[3], w[2], q & 7u);
+        return (q & 8u) ? hi : lo;
+    };
+    const bool bad1 = c1 < 16u && (byte_at(c1) & 0xFFu) != 0x32u;
+    const bool bad2 = c2 < 16u && (byte_at(c2) & 0xFFu) != 0x32u;
+    r.reject = bad1 || bad2 || (lane < kOwnLanes && __builtin_popcount(r.del) > 2);
+    const u32 K = lane < kOwnLanes ? (~r.del & 0xFFFFu) : ((prevP >> 15) & 1u);
+    r.kept = (u32)__builtin_popcount(K);
+    const u32 nd = lane < kOwnLanes ? (u32)__builtin_popcount(r.del) : 0u;
+    const uint64_t B1 = __builtin_amdgcn_ballot_w64(nd >= 1u), B2 = __builtin_amdgcn_ballot_w64(nd >= 2u);
+    const uint64_t B3 = __builtin_amdgcn_ballot_w64(lane == kWave - 1u && r.kept != 0u);
+    r.oexcl = 16u * lane - (__builtin_amdgcn_mbcnt_hi((u32)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((u32)B1, 0u)) +
+                            __builtin_amdgcn_mbcnt_hi((u32)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((u32)B2, 0u)));
+    r.ttot = 16u * kOwnLanes - (u32)__builtin_popcountll(B1) - (u32)__builtin_popcountll(B2) + (u32)(B3 >> 63);
+    return r;
+}
+// The tile's bytes with its deleted positions removed, stored at base + the lane's offset (the last
+// lane's bytes past the tile's output are rewritten by later stores of this wave).
+__device__ __forceinline__ void dec_lit_emit(const DecPrep& pr, const DecLit& f, u32 lane, const u32x4* clut, u32x4 rso,
+                                             u32 base, bool wt) {
+    const u32* w = pr.w;
+    const u32 dm = lane < kOwnLanes ? f.del : 0u;
+    const u32 t1 = (u32)__builtin_ctz(dm | 0x10000u);
+    const u32 t2 = (u32)__builtin_ctz((dm & (dm - 1u)) | 0x10000u);
+    u32 y[4] = {w[0], w[1], w[2], w[3]};
+    if (__builtin_amdgcn_ballot_w64(t2 < 16u)) {
+        const u32x4 s2 = clut[t2];
+        const u32 y3 = __builtin_amdgcn_perm(y[3], y[3], s2.w);
+        y[0] = __builtin_amdgcn_perm(y[1], y[0], s2.x);
+        y[1] = __builtin_amdgcn_perm(y[2], y[1], s2.y);
+        y[2] = __builtin_amdgcn_perm(y[3], y[2], s2.z);
+        y[3] = y3;
+    }
+    const u32x4 sel = clut[t1];
+    u32x4 o;
+    o.x = __builtin_amdgcn_perm(y[1], y[0], sel.x);
+    o.y = __builtin_amdgcn_perm(y[2], y[1], sel.y);
+    o.z = __builtin_amdgcn_perm(y[3], y[2], sel.z);
+    const u32 c3 = __builtin_amdgcn_perm(y[3], y[3], sel.w);
+    const u32 n0 = from_next_lane(o.x, 0u);
+    const u32 s3 = f.kept >= 16u ? 0x03020100u : f.kept == 15u ? 0x04020100u : 0x05040100u;
+    o.w = lane < kOwnLanes ? __builtin_amdgcn_perm(n0, c3, s3) : c3;
+    vstore(rso, f.kept ? base + f.oexcl : kOOB, o, wt);
+}
+#ifndef RLE_DEC_PAIR   // 1: the one-round decode kernel walks two tiles per step (dec_pair)
+#define RLE_DEC_PAIR 1
+#endif
+// Tiles at pos (slot A) and pos + 1008 (slot B).  Returns the store instructions issued after both
+// refills, or ~0u (the stream needs the exact serial path).
+template <u32 kChunks, bool kUni>
+__device__ __forceinline__ u32 dec_pair(const uint8_t* slotA, const uint8_t* slotB, const Refill& nxA, const Refill& nxB,
+                                        u32 pos, u32 C, u32 U, u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst,
+                                        u32x4 rso, DecState& st, const DecK& kc, const u32x4* clut) {
+    constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+    const u32x4 curA = *reinterpret_cast<const u32x4*>(slotA + 16u * lane);
+    const u32x4 curB = *reinterpret_cast<const u32x4*>(slotB + 16u * lane);
+    nxA();
+    nxB();
+    const u32 posB = pos + kTileStep;
+    const DecPrep prA = dec_prepare(curA, pos, C, C, lane, tbl, kc);
+    const DecPrep prB = dec_prepare(curB, posB, C, C, lane, tbl, kc);
+    if (RLE_DEC_FAST && !st.head && !prB.tail) {   // (prA.tail implies prB.tail)
+        const u32 NEa = (prA.xa >> 7) | (prA.xb << 1), NEb = (prB.xa >> 7) | (prB.xb << 1);
+        // cheap reject first (runs): at most 2 equal neighbours per owned lane, in both tiles
+        if (!(__builtin_amdgcn_ballot_w64(__builtin_popcount(~NEa & 0xFFFFu) > 2 ||
+                                          __builtin_popcount(~NEb & 0xFFFFu) > 2) & kOwned)) {
+            const u32 dA = st.d;
+            const u32 dB = bfe(readlane(prA.incl, kOwnLanes - 1u), 8u * dA, 8);
+            const DecLit a = dec_lit_an(prA, lane, dA);
+            const DecLit b = dec_lit_an(prB, lane, dB);
+            if (!__builtin_amdgcn_ballot_w64(a.reject || b.reject) && st.out_pos + a.ttot + b.ttot + 16u <= U) {
+                u32 rounds = 2u;
+                const u32 rel0 = st.out_pos - st.flushed;
+                if (rel0) {   // a general tile's partial chunk: store it (its bytes past rel0 are rewritten below)
+                    u32x4 x, y;
+                    dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), x, y);
+                    u32 L[8];
+                    dec_fill_scan(x, y, L);
+                    vstore(rso, lane == 0u ? st.flushed : kOOB, dec_fill_out(L, st.fillc), st.wt);
+                    wave_lds_sync();
+                    if (lane < 8u)
+                        *reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane)) = 0u;
+                    wave_lds_sync();
+                    ++rounds;
+                }
+                dec_lit_emit(prA, a, lane, clut, rso, st.out_pos, st.wt);
+                dec_lit_emit(prB, b, lane, clut, rso, st.out_pos + a.ttot, st.wt);
+                st.out_pos += a.ttot + b.ttot;
+                st.flushed = st.out_pos;
+                st.d = bfe(readlane(prB.incl, kOwnLanes - 1u), 8u * dB, 8);
+                st.prev = readlane(prB.w[3], kOwnLanes - 1u);
+                st.vrun = 0u;
+                st.sv = false;
+                return rounds;
+            }
+        }
+    }
+    // one after the other (dec_tile's uniform-tile test included)
+    auto one = [&](const u32x4 cur, const DecPrep& pr, u32 p) -> u32 {
+        if (kUni && RLE_DEC_UNIFORM && !(RLE_ABL & 32) && (st.sv || !RLE_DEC_UNIFORM_GATE) && !st.head &&
+            p + kSlot + 2u <= C && st.out_pos + kUniformOut <= U) {
+            u32 v;
+            if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
+                const u32 r = dec_fill_run(v, kUniformOut, lane, stage, rso, st);
+                st.prev = readlane(cur.w, kOwnLanes - 1u);
+                return r;
+            }
+        }
+        return dec_tile_pr<true, kChunks>(pr, p, C, C, U, lane, stage, dst, rso, st, kc, clut);
+    };
+    const u32 r0 = one(curA, prA, pos);
+    if (r0 == ~0u) return ~0u;
+    const u32 r1 = one(curB, prB, posB);
+    if (r1 == ~0u) return ~0u;
+    return r0 + r1;
+}
+
 // After the last tile: outputs [flushed, end) = the partial chunk still staged (decoded positions
 // < out_pos), then zeros or the final unbounded token's byte (end = U for a stream's last segment,
 // end = out_pos for the others).  Bytes below flushed + head belong to the previous segment.

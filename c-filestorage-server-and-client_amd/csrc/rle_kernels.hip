@@ -432,7 +432,15 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                 cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
         };
         bool serial;
-        if constexpr (kDepth == 2u) serial = walk_tiles(rsi, 0u, ntiles, lane, slots, tile, true);
+        constexpr bool kUniK = (kChunks >= 191u ? RLE_DEC_UNIFORM_ONE : RLE_DEC_UNIFORM_LARGE) != 0;
+        if constexpr (kDepth == 2u && kChunks >= 191u && RLE_DEC_PAIR)   // one round: two tiles per step
+            serial = walk_pairs(rsi, 0u, ntiles, lane, slots,
+                                [&](u32 t, const uint8_t* sa, const uint8_t* sb, const Refill& na, const Refill& nb) {
+                                    return dec_pair<kChunks, kUniK>(sa, sb, na, nb, t * kTileStep, C, U, lane, tbl, stage,
+                                                                    dst, rso, st, kc, clut);
+                                },
+                                tile, true);
+        else if constexpr (kDepth == 2u) serial = walk_tiles(rsi, 0u, ntiles, lane, slots, tile, true);
         else serial = walk_ring<kDepth>(rsi, 0u, ntiles, lane, slots, tile);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;

@@ -395,3 +395,38 @@ def test_encode_tile_pairs_match_oracle():
             x[a:b] = bytes([int(rng.integers(0, 256))]) * (b - a)
         xs.append(bytes(x))
     _oracle_parity(xs)
+
+
+def test_decode_tile_pairs_match_oracle():
+    """Two decode tiles per step in the one-round kernel (csrc/rle_device.h dec_pair): streams built
+    tile by tile from literal stretches ("vv2" pairs, the fast path's tiles) and general stretches
+    (a count other than 2, or run tokens), in every pattern of 1..9 tiles, so that every pair is
+    literal + literal, literal + general, general + literal (a staged partial chunk handed to a
+    literal pair) or general + general, the last tile of an odd count alone, and the last tile a
+    tail; shifted by 0..4 bytes so that tokens straddle the pair's and the tiles' edges.  Decoded in
+    one batch (one-round kernel) at the exact size, a larger one (SHORT) and a smaller one (the serial
+    path), against the oracle."""
+    rng = np.random.default_rng(4242)
+    streams = []
+    for nt in range(1, 10):
+        for pat in range(min(1 << nt, 48)):
+            bits = pat if nt <= 5 else int(rng.integers(0, 1 << nt))
+            for shift in (0, 1, 2, 3, 4) if nt <= 4 else (int(rng.integers(0, 5)),):
+                parts = [bytes(range(1, 1 + shift))]
+                for t in range(nt):
+                    general = (bits >> t) & 1
+                    n = STEP - (int(rng.integers(0, 40)) if t == nt - 1 else 0)
+                    s, _ = _stream(rng, n, 0.06, 0.01 if general else 0.0, 0.002 if general else 0.0)
+                    if general:   # at least one "vv5" token in the tile
+                        s = s[:200] + bytes([0x37, 0x37, ord("5")]) + s[203:] if s[199] != 0x37 else s
+                    parts.append(s[:n])
+                streams.append(b"".join(parts))
+    # a token boundary is not preserved across the parts' joins: decode whatever the bytes parse to
+    sizes = [_natural_size(s) for s in streams]
+    assert len(streams) <= 4096
+    for delta in (0, 9, -4):
+        us = [max(0, u + delta) for u in sizes]
+        dec, st = gpu_decode(streams, us)
+        for i, s in enumerate(streams):
+            ref, rst = O.decode(s, us[i])
+            assert dec[i] == ref, (delta, i, len(s), us[i])
