@@ -2206,7 +2206,7 @@ __device__ __forceinline__ void dec_lit_emit(const DecPrep& pr, const DecLit& f,
     vstore(rso, f.kept ? base + f.oexcl : kOOB, o, wt);
 }
 #ifndef RLE_DEC_PAIR   // 1: the one-round decode kernel walks two tiles per step (dec_pair)
-#define RLE_DEC_PAIR 1
+#define RLE_DEC_PAIR 0   // r5r same process: configs[1] decode 9.39 -> 9.93 us with it (lone waves -2 %)
 #endif
 // Tiles at pos (slot A) and pos + 1008 (slot B).  Returns the store instructions issued after both
 // refills, or ~0u (the stream needs the exact serial path).

@@ -46,6 +46,9 @@ constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the w
 #ifndef RLE_SEG_REVERSE   // the write passes take the segments last-summarised first (memory-side cache reuse)
 #define RLE_SEG_REVERSE 1   // r3w, same process: configs[2] mixed batch encode -6 %, decode -2 %; 1 MiB kinds +-1 %
 #endif
+#ifndef RLE_SEG_SUMDEFER   // 1: a decode summary sums its lanes' counts once per segment, not per tile
+#define RLE_SEG_SUMDEFER 1
+#endif
 #ifndef RLE_SEG_SUMFAST   // the summaries count uniform / literal tiles without the full analysis (round 3)
 #define RLE_SEG_SUMFAST 1
 #endif
@@ -192,6 +195,7 @@ __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u3
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     u32 prev_top = p0 ? (u32)src[p0 - 1u] << 24 : 0u;
     u32 rs = p0, fb = kNone, lb = kNone, rest = 0;
+    u32 restl = 0u, lbl = 0u;   // RLE_SEG_SUMDEFER: the lane's token bytes and its last boundary + 1 (0: none)
     const EncK kc = enc_k();
     walk_seg<kRes>(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
@@ -223,23 +227,39 @@ __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u3
         const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, pos, U, p1, lane, prev_top, rs, kc);
         // run boundaries inside the segment: the first one (L0) and the last one (lb)
         const u32 Bo = an.B & an.validm;
-        const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
-        if (bl) {
-            const u32 fl = (u32)__builtin_ctzll(bl), ll = 63u - (u32)__builtin_clzll(bl);
-            const u32 first = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), fl);
-            const u32 last = readlane(an.p0 + 31u - (u32)__builtin_clz(Bo | 1u), ll);
-            if (fb == kNone) fb = first;
-            lb = last;
+        if (RLE_SEG_SUMDEFER) {
+            // the first boundary on the scalar unit until found; the last one per lane (tiles come in
+            // order, so a lane's latest is its last), the lanes' maximum taken once per segment
+            if (fb == kNone) {
+                const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
+                if (bl) fb = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), (u32)__builtin_ctzll(bl));
+            }
+            lbl = Bo ? an.p0 + 32u - (u32)__builtin_clz(Bo) : lbl;
+        } else {
+            const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
+            if (bl) {
+                const u32 fl = (u32)__builtin_ctzll(bl), ll = 63u - (u32)__builtin_clzll(bl);
+                const u32 first = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), fl);
+                const u32 last = readlane(an.p0 + 31u - (u32)__builtin_clz(Bo | 1u), ll);
+                if (fb == kNone) fb = first;
+                lb = last;
+            }
         }
         // tokens at or after the first boundary do not depend on the entering run phase
         u32 fbm = 0u;
         if (fb != kNone) fbm = fb <= an.p0 ? 0xFFFFu : (fb >= an.p0 + 16u ? 0u : ~lowmask(fb - an.p0) & 0xFFFFu);
-        rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
+        if (RLE_SEG_SUMDEFER) restl += bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u);
+        else rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
         prev_top = readlane(an.top, kOwnLanes - 1u);
         const u32 i63 = readlane(an.incl, kOwnLanes - 1u);
         rs = i63 > rs ? i63 : rs;
         return 0u;
     });
+    if (RLE_SEG_SUMDEFER) {
+        rest += wave_sum(restl);
+        const u32 m = readlane(wave_scan_incl(lbl, 0u, OpMax()), kWave - 1u);
+        if (m) lb = m - 1u;
+    }
     const u32 L0 = fb == kNone ? p1 - p0 : fb - p0;
     const u32 cont = (fb == kNone && p1 < U && src[p1] == src[p1 - 1u]) ? 1u : 0u;
     return make_uint4(L0, lb == kNone ? 0u : lb + 1u, rest, cont);
@@ -739,6 +759,8 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
 // literal path's count, dec_tile_fast, without its stores or its per-lane limits).  kNotFast when a
 // pair has another count (the caller then runs dec_lengths).  About 40 VALU against ~100 for
 // dec_lengths + its sum.
+// kLane: the lane's own count (the caller sums the lanes once per segment, RLE_SEG_SUMDEFER).
+template <bool kLane = false>
 __device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 lane, const DecK& kc) {
     constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
     const u32* w = pr.w;
@@ -766,7 +788,7 @@ __device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 l
     if (lane == 0u) del |= lowmask(d);
     const u32 K = lane < kOwnLanes ? (~del & 0xFFFFu) : ((prevP >> 15) & 1u);
     if (__builtin_amdgcn_ballot_w64((P16 & NZ16) != 0u) & kOwned) return kNotFast;
-    return wave_sum((u32)__builtin_popcount(K));
+    return kLane ? (u32)__builtin_popcount(K) : wave_sum((u32)__builtin_popcount(K));
 }
 
 // One segment's decode summary: for each entry phase 0..2, the decoded bytes (.x .y .z) and, in .w,
@@ -795,6 +817,8 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
     u32 uni = RLE_SEG_UNIFORM ? 7u : 0u, v0 = 0u, v1 = 0u, v2 = 0u;   // single-byte phases and their bytes
+    u32 accm = 0u;       // RLE_SEG_SUMDEFER: the lane's decoded bytes over the tiles after the phases merged
+    bool badl = false;   // ... and whether the lane declined in one of them
     const DecK kc = dec_k();
     walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
@@ -802,12 +826,17 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
         const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
         const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
         if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
-            u32 tot = (RLE_SEG_SUMFAST && !pr.tail) ? dec_count_literal(pr, d0, lane, kc) : kNotFast;
+            u32 tot = (RLE_SEG_SUMFAST && !pr.tail) ? dec_count_literal<RLE_SEG_SUMDEFER>(pr, d0, lane, kc) : kNotFast;
             bool bad = false;
             if (tot == kNotFast) {
                 const DecLen ln = dec_lengths(pr, d0);
-                tot = owned_sum(ln.nout);
-                bad = owned_any(ln.serial_lane);
+                if (RLE_SEG_SUMDEFER) {   // the lane's count and decline, summed once per segment
+                    tot = lane < kOwnLanes ? ln.nout : 0u;
+                    badl |= lane < kOwnLanes && ln.serial_lane;
+                } else {
+                    tot = owned_sum(ln.nout);
+                    bad = owned_any(ln.serial_lane);
+                }
                 if (uni) {
                     u32 v;
                     const bool one = dec_tile_single(pr, ln, d0, kc, v);
@@ -818,8 +847,12 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
             } else {
                 uni = 0u;   // a literal tile (its own bytes, "v v 2" pairs): not counted as single-byte
             }
-            c0 += tot; c1 += tot; c2 += tot;
-            badm |= bad ? 7u : 0u;
+            if (RLE_SEG_SUMDEFER) {
+                accm += tot;
+            } else {
+                c0 += tot; c1 += tot; c2 += tot;
+                badm |= bad ? 7u : 0u;
+            }
             d0 = d1 = d2 = bfe(m63, 8u * d0, 8);
         } else {
             const DecLen l0 = dec_lengths(pr, d0);
@@ -849,6 +882,11 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
         }
         return 0u;
     });
+    if (RLE_SEG_SUMDEFER) {
+        const u32 cm = wave_sum(accm);
+        c0 += cm; c1 += cm; c2 += cm;
+        badm |= __builtin_amdgcn_ballot_w64(badl) ? 7u : 0u;
+    }
     return make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8) | (uni << 11));
 }
 // the summary of an empty stream: counts 0, exit = entry
