@@ -290,6 +290,56 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
     }
 }
 
+// Issue order in one launch and without global counts (RLE_ORDER_LOCAL, round 5): each workgroup sorts
+// its own kOrderChunk buffers longest first (its LDS histogram, a descending scan of it, each buffer's
+// place = its bucket's start + its rank in the bucket) into order[chunk * kOrderChunk ...], and the
+// decode kernel interleaves the F = n / kOrderChunk full chunks (slot s takes place s / F of chunk
+// s % F; the last partial chunk follows them): the i-th heaviest buffers of every chunk are issued
+// together, which on batches whose chunks hold similar mixes (every bench and server batch) is the
+// global longest-first order without the memset, the second launch and the global atomics.
+__global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
+                                                              uint32_t* __restrict__ order) {
+    __shared__ u32 lh[kOrderBuckets];
+    __shared__ u32 wsum[4];
+    constexpr u32 kPerT = kOrderBuckets / 256u;
+    const u32 t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+    u32 key[kOrderPer], rank[kOrderPer];
+    order_local(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
+    // thread t: the 8 buckets from B-1-8t down, in descending bucket order
+    u32 c[kPerT], sum = 0u;
+#pragma unroll
+    for (u32 j = 0; j < kPerT; ++j) {
+        c[j] = lh[kOrderBuckets - 1u - (kPerT * t + j)];
+        sum += c[j];
+    }
+    const u32 incl = wave_scan_incl(sum, 0u, OpAdd());
+    if (lane == kWave - 1) wsum[wv] = incl;
+    __syncthreads();   // (every thread has read its counts: lh may be overwritten below)
+    u32 base = incl - sum;
+    for (u32 w = 0; w < wv; ++w) base += wsum[w];
+#pragma unroll
+    for (u32 j = 0; j < kPerT; ++j) {
+        lh[kOrderBuckets - 1u - (kPerT * t + j)] = base;
+        base += c[j];
+    }
+    __syncthreads();
+    const u32 i0 = blockIdx.x * kOrderChunk + threadIdx.x;
+#pragma unroll
+    for (u32 j = 0; j < kOrderPer; ++j) {
+        const u32 i = i0 + 256u * j;
+        if (i < n) order[blockIdx.x * kOrderChunk + lh[key[j]] + rank[j]] = i;
+    }
+}
+#ifndef RLE_ORDER_LOCAL
+#define RLE_ORDER_LOCAL 1
+#endif
+// The buffer a decode wave takes at issue slot s of an order made by dec_order_local_kernel.
+__device__ __forceinline__ u32 order_slot_local(u32 s, u32 n) {
+    const u32 F = n / kOrderChunk;   // full chunks, interleaved; the partial one after them
+    if (s >= F * kOrderChunk) return s;
+    return (s % F) * kOrderChunk + s / F;
+}
+
 // kChunks: staging chunks per wave (32 B each).  192 hold any tile's output in one pass; the
 // launcher takes 96 (3 KiB per wave: 7 workgroups per CU instead of 4) for batches past one
 // residency round, where the extra waves hide more latency than the two-pass staging of the
@@ -356,6 +406,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         } else if (RLE_ORDER_MODE == 2 && slot < n) {
             slot = (slot & 1u) ? n - 1u - (slot >> 1) : (slot >> 1);
         }
+        if (RLE_ORDER_LOCAL && slot < n) slot = uniform(order_slot_local(slot, n));
         b = slot < n ? uniform(order[slot]) : n;
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
@@ -647,12 +698,16 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     const hipStream_t s = (hipStream_t)stream;
     // more buffers than one residency round: issue them longest first (rle::dec_order_kernel)
     uint32_t* order = nullptr;   // [n] issue order, then [kOrderBuckets] counts and cursors
+    constexpr size_t kOrderExtra = RLE_ORDER_LOCAL ? 0u : 2u * rle::kOrderBuckets;
     if (n > kDecRound && dec_order_enabled() &&
-        hipMallocAsync((void**)&order, sizeof(uint32_t) * ((size_t)n + 2u * rle::kOrderBuckets), s) != hipSuccess) {
+        hipMallocAsync((void**)&order, sizeof(uint32_t) * ((size_t)n + kOrderExtra), s) != hipSuccess) {
         (void)hipGetLastError();
         order = nullptr;
     }
-    if (order) {
+    if (order && RLE_ORDER_LOCAL) {   // one launch, chunk-local sorts (rle::dec_order_local_kernel)
+        hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kOrderChunk - 1u) / rle::kOrderChunk), dim3(256), 0,
+                           s, d_in_len, n, order);
+    } else if (order) {
         uint32_t* hist = order + n;
         uint32_t* cursor = hist + rle::kOrderBuckets;
         const dim3 g((n + rle::kOrderChunk - 1u) / rle::kOrderChunk);
