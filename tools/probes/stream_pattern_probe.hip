@@ -81,6 +81,48 @@ __global__ __launch_bounds__(256) void per_wave(const uint8_t* in, uint8_t* out,
     }
 }
 
+
+// The same with kBurst consecutive 1 KiB tiles per step: a wave's loads reach the memory as
+// kBurst-KiB contiguous bursts (and its stores as kOut * kBurst KiB).
+template <u32 kOut, u32 kDepth, u32 kPad, u32 kBurst>
+__global__ __launch_bounds__(256) void per_wave_burst(const uint8_t* in, uint8_t* out, u32 nbuf, u32 inb) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots[4 * kDepth * kBurst * 1024 + kPad];
+    const u32 lane = threadIdx.x & 63, wid = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const u32 b = blockIdx.x * 4 + wid;
+    if (kPad && threadIdx.x == 0) ((volatile uint8_t*)slots)[4 * kDepth * kBurst * 1024] = 0;
+    if (b >= nbuf) return;
+    const u32x4 ri = rsrc(in + (uint64_t)b * inb, inb);
+    const u32x4 ro = rsrc(out + (uint64_t)b * inb * kOut, inb * kOut);
+    uint8_t* my = slots + wid * kDepth * kBurst * 1024;
+    const u32 l0 = (u32)__builtin_amdgcn_readfirstlane((int)lds_addr(my));
+    const u32 nt = inb / (1024u * kBurst);   // steps
+    constexpr u32 kSt = kBurst * 1024u;
+    asm volatile("s_nop 4" ::: "memory");
+    for (u32 d = 0; d < kDepth && d < nt; ++d)
+        for (u32 q = 0; q < kBurst; ++q) dma(ri, kSt * d + 1024u * q + 16u * lane, l0 + kSt * d + 1024u * q);
+    for (u32 t = 0; t < nt; ++t) {
+        u32 after = 0;
+        if (t < kDepth) {
+            for (u32 k = t + 1u; k < kDepth; ++k) after += k < nt ? kBurst : 0u;
+            for (u32 j = 0; j < t; ++j) after += (j + kDepth < nt ? kBurst : 0u) + kOut * kBurst;
+        } else {
+            after += kOut * kBurst;
+            for (u32 j = t - kDepth + 1u; j < t; ++j) after += (j + kDepth < nt ? kBurst : 0u) + kOut * kBurst;
+        }
+        vmw(after);
+        const u32 s = t % kDepth;
+        u32x4 v[kBurst];
+#pragma unroll
+        for (u32 q = 0; q < kBurst; ++q) v[q] = *reinterpret_cast<const u32x4*>(my + s * kSt + 1024u * q + 16u * lane);
+        if (t + kDepth < nt)
+            for (u32 q = 0; q < kBurst; ++q) dma(ri, kSt * (t + kDepth) + 1024u * q + 16u * lane, l0 + kSt * s + 1024u * q);
+#pragma unroll
+        for (u32 q = 0; q < kBurst; ++q)
+#pragma unroll
+            for (u32 o = 0; o < kOut; ++o) st16(ro, kOut * kSt * t + 1024u * (kOut * q + o) + 16u * lane, v[q] + o);
+    }
+}
+
 __global__ void strided(u32x4* dst, const u32x4* src, uint64_t n16, uint64_t m16) {
     const uint64_t stride = (uint64_t)gridDim.x * 1024u;
     for (uint64_t base = (uint64_t)blockIdx.x * 1024u + threadIdx.x; base < n16; base += stride) {
@@ -122,6 +164,14 @@ static void run(const char* name, const uint8_t* in, uint8_t* out, u32 nbuf, u32
     printf("%-34s out/in %u depth %u pad %6u: %8.1f us  %.2f TB/s\n", name, kOut, kDepth, kPad, ms * 1e3, bytes / ms / 1e9);
 }
 
+
+template <u32 kOut, u32 kDepth, u32 kPad, u32 kBurst>
+static void runb(const char* name, const uint8_t* in, uint8_t* out, u32 nbuf, u32 inb) {
+    const float ms = timeit([&] { hipLaunchKernelGGL((per_wave_burst<kOut, kDepth, kPad, kBurst>), dim3((nbuf + 3) / 4), dim3(256), 0, 0, in, out, nbuf, inb); }, 10);
+    const double bytes = (double)nbuf * inb * (1 + kOut);
+    printf("%-34s out/in %u depth %u burst %u pad %6u: %8.1f us  %.2f TB/s\n", name, kOut, kDepth, kBurst, kPad, ms * 1e3, bytes / ms / 1e9);
+}
+
 int main() {
     const u32 nbuf = 16384, inb = 65536;
     uint8_t *in, *out;
@@ -137,6 +187,10 @@ int main() {
     run<3, 2, 0>("per-wave 1:3 (16 WG/CU cap)", in, out, nbuf, inb / 3 / 1024 * 1024);
     run<3, 2, 14000>("per-wave 1:3 (~7 WG/CU)", in, out, nbuf, inb / 3 / 1024 * 1024);
     run<3, 4, 6000>("per-wave 1:3 depth 4 (~7 WG/CU)", in, out, nbuf, inb / 3 / 1024 * 1024);
+    runb<1, 2, 6000, 2>("burst 2 KiB 1:1 (~7 WG/CU)", in, out, nbuf, inb);
+    runb<1, 2, 0, 4>("burst 4 KiB 1:1 (~5 WG/CU)", in, out, nbuf, inb);
+    runb<1, 2, 0, 2>("burst 2 KiB 1:1 (~10 WG/CU)", in, out, nbuf, inb);
+    runb<3, 2, 2000, 2>("burst 2 KiB 1:3 (~7 WG/CU)", in, out, nbuf, inb / 3 / 2048 * 2048);
     {
         const uint64_t n16 = (uint64_t)nbuf * inb / 16;
         const float ms = timeit([&] { hipLaunchKernelGGL(strided, dim3(4096), dim3(256), 0, 0, (u32x4*)out, (const u32x4*)in, n16, n16); }, 10);
