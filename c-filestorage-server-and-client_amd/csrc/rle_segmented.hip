@@ -123,6 +123,20 @@ __global__ __launch_bounds__(kMapBlock) void seg_map_kernel(const u32* __restric
     }
     seg_buf[g] = lo;
 }
+// A launch of one buffer (the drop-in's single large calls) skips the plan and map launches: the
+// launcher passes seg_first = seg_buf = nullptr, and every segment is buffer 0's, its segments
+// [0, seg_count(in_len[0])) (RLE_SEG_ONE).
+#ifndef RLE_SEG_ONE
+#define RLE_SEG_ONE 1
+#endif
+__device__ __forceinline__ u32 seg_total(const u32* seg_first, u32 n, const uint64_t* len, u32 sb) {
+    return seg_first ? uniform(seg_first[n]) : seg_count(len32(len[0]), sb);
+}
+__device__ __forceinline__ u32 seg_of(const u32* seg_buf, u32 g) { return seg_buf ? uniform(seg_buf[g]) : 0u; }
+__device__ __forceinline__ u32 seg_lo(const u32* seg_first, u32 b) { return seg_first ? uniform(seg_first[b]) : 0u; }
+__device__ __forceinline__ u32 seg_hi(const u32* seg_first, u32 b, const uint64_t* len, u32 sb) {
+    return seg_first ? uniform(seg_first[b + 1]) : seg_count(len32(len[0]), sb);
+}
 __device__ __forceinline__ void seg_range(u32 i, u32 nseg, u32 n, u32 sb, u32& p0, u32& p1) {
     p0 = i * sb;
     p1 = (i + 1u == nseg) ? n : p0 + sb;
@@ -274,11 +288,11 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_summary_kernel(const uint8_
     const u32 lane = threadIdx.x & (kWave - 1);
     const u32 wid = uniform(threadIdx.x / kWave);
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    u32 total = uniform(seg_first[n]);
+    u32 total = seg_total(seg_first, n, in_len, sb);
     total = total < maxseg ? total : maxseg;
     for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
-        const u32 b = uniform(seg_buf[g]);
-        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const u32 b = seg_of(seg_buf, g);
+        const u32 s0 = seg_lo(seg_first, b), nseg = seg_hi(seg_first, b, in_len, sb) - s0;
         const uint64_t U64 = in_len[b];
         const uint8_t* src = in + in_off[b];
         uint4 res = make_uint4(0u, 0u, 0u, 0u);
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_scan_kernel(const uint8_t* 
     const uint64_t U64 = in_len[b];
     const uint8_t* src = in + in_off[b];
     uint8_t* dst = out + out_off[b];
-    const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]);
+    const u32 s0 = seg_lo(seg_first, b), s1 = seg_hi(seg_first, b, in_len, sb);
     u32 bad = (((uintptr_t)src | (uintptr_t)dst) & 15u) ? RLE_STATUS_MISALIGNED : 0u;
     if (U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
     if (bad) {
@@ -463,16 +477,16 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
     for (u32 k = threadIdx.x; k < kInsWaveWords; k += kSegBlock) elut[k] = kEncInsLut.s[k];
     __syncthreads();
-    u32 total = uniform(seg_first[n]);
+    u32 total = seg_total(seg_first, n, in_len, sb);
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
         const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
         // (the segment's own plan and summary load with its buffer index, not after it)
         const uint2 pl = plan[g];
         const uint4 sm = RLE_SEG_UNIFORM ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
-        const u32 b = uniform(seg_buf[g]);
+        const u32 b = seg_of(seg_buf, g);
         if (uniform(bflag[b])) continue;
-        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const u32 s0 = seg_lo(seg_first, b), nseg = seg_hi(seg_first, b, in_len, sb) - s0;
         const u32 U = (u32)in_len[b];
         const uint8_t* src = in + in_off[b];
         uint8_t* dst = out + out_off[b];
@@ -904,11 +918,11 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_summary_kernel(const uint8_
     for (u32 k = threadIdx.x; k < 256u; k += kSegBlock) tbl[k] = dec_entry_from(kDecTable.e[k]);
     __syncthreads();
     const uint8_t* slots = slots_all + wid * 2 * kSlot;
-    u32 total = uniform(seg_first[n]);
+    u32 total = seg_total(seg_first, n, in_len, sb);
     total = total < maxseg ? total : maxseg;
     for (u32 g = blockIdx.x * kSegWaves + wid; g < total; g += gridDim.x * kSegWaves) {
-        const u32 b = uniform(seg_buf[g]);
-        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const u32 b = seg_of(seg_buf, g);
+        const u32 s0 = seg_lo(seg_first, b), nseg = seg_hi(seg_first, b, in_len, sb) - s0;
         const uint64_t C64 = in_len[b];
         const uint8_t* src = in + in_off[b];
         uint4 res = kDecEmpty;
@@ -965,7 +979,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_scan_kernel(const uint8_t* 
     const uint64_t cap = out_cap ? out_cap[b] : U64;
     const uint8_t* src = in + in_off[b];
     uint8_t* dst = out + out_off[b];
-    const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]);
+    const u32 s0 = seg_lo(seg_first, b), s1 = seg_hi(seg_first, b, in_len, sb);
     u32 bad = ((((uintptr_t)src | (uintptr_t)dst) & 15u) || cap < U64) ? RLE_STATUS_MISALIGNED : 0u;
     if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes || s1 > maxseg) bad |= RLE_STATUS_TOOLARGE;
     if (bad) {
@@ -1053,16 +1067,16 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
     for (u32 k = lane; k < kStage / 16u; k += kWave)
         reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
-    u32 total = uniform(seg_first[n]);
+    u32 total = seg_total(seg_first, n, in_len, sb);
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
         const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
         const uint2 pl = plan[g];
         const uint4 sm = RLE_SEG_UNIFORM ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
-        const u32 b = uniform(seg_buf[g]);
+        const u32 b = seg_of(seg_buf, g);
         const u32 flag = uniform(bflag[b]);
         if (flag & kFlagSkip) continue;
-        const u32 s0 = uniform(seg_first[b]), nseg = uniform(seg_first[b + 1]) - s0;
+        const u32 s0 = seg_lo(seg_first, b), nseg = seg_hi(seg_first, b, in_len, sb) - s0;
         const u32 C = (u32)in_len[b], U = (u32)out_len[b];
         const uint8_t* src = in + in_off[b];
         uint8_t* dst = out + out_off[b];
@@ -1379,16 +1393,22 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     }
 #endif
     const uint32_t grid = seg_grid(maxseg, ncu);
-    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
-                       nullptr, nullptr);
-    hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n, maxseg,
-                       w.seg_buf);
+    // one buffer: no plan / map launches, the kernels take its segments from its length (RLE_SEG_ONE)
+    const bool one = RLE_SEG_ONE && n == 1u;
+    uint32_t* const seg_first = one ? nullptr : w.seg_first;
+    uint32_t* const seg_buf = one ? nullptr : w.seg_buf;
+    if (!one) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
+                           nullptr, nullptr);
+        hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
+                           maxseg, w.seg_buf);
+    }
     hipLaunchKernelGGL(rle::enc_seg_summary_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, n,
-                       w.seg_first, w.seg_buf, maxseg, sb, w.summ);
+                       seg_first, seg_buf, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::enc_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
-                       out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
+                       out, d_out_off, d_out_len, d_status, n, seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
     hipLaunchKernelGGL(rle::enc_seg_write_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out,
-                       d_out_off, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag, w.summ);
+                       d_out_off, n, seg_first, seg_buf, maxseg, sb, w.plan, w.bflag, w.summ);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 
@@ -1424,14 +1444,19 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     }
 #endif
     const uint32_t grid = seg_grid(maxseg, ncu);
-    hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
-                       nullptr, nullptr);
-    hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n, maxseg,
-                       w.seg_buf);
+    const bool one = RLE_SEG_ONE && n == 1u;   // (as in the encode: no plan / map launches for one buffer)
+    uint32_t* const seg_first = one ? nullptr : w.seg_first;
+    uint32_t* const seg_buf = one ? nullptr : w.seg_buf;
+    if (!one) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
+                           nullptr, nullptr);
+        hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
+                           maxseg, w.seg_buf);
+    }
     hipLaunchKernelGGL(rle::dec_seg_summary_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, n,
-                       w.seg_first, w.seg_buf, maxseg, sb, w.summ);
+                       seg_first, seg_buf, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::dec_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
-                       out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
+                       out, d_out_off, d_out_len, d_out_cap, d_status, n, seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
 #ifndef RLE_SEG_DEC_FORCE   // A/B builds: 96 or 192 forces the decode write pass's staging
 #define RLE_SEG_DEC_FORCE 0
 #endif
@@ -1440,6 +1465,6 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     hipLaunchKernelGGL(one_round ? rle::dec_seg_write_kernel<rle::kSegDecChunksOne>
                                  : rle::dec_seg_write_kernel<rle::kSegDecChunksMany>,
                        dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out, d_out_off, d_out_len,
-                       d_out_cap, d_status, n, w.seg_first, w.seg_buf, maxseg, sb, w.plan, w.bflag, w.summ);
+                       d_out_cap, d_status, n, seg_first, seg_buf, maxseg, sb, w.plan, w.bflag, w.summ);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
