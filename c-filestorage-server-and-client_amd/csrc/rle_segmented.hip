@@ -61,17 +61,12 @@ __device__ __forceinline__ u32 seg_count(u32 n, u32 sb) {
 }
 __device__ __forceinline__ u32 len32(uint64_t n) { return n > kMaxBufferBytes ? 0u : (u32)n; }
 
-// seg_first[i] = segments of buffers < i; seg_first[n] = total.  One workgroup.  With seg_buf (and
-// n < kPlanLds) it also writes each segment's buffer, seg_map_kernel's work, from an LDS copy of
-// seg_first: thread t takes a contiguous range of segments, one binary search for its first and
-// then a walk (one launch fewer per segmented call, r5y).
-constexpr u32 kPlanLds = 4096;
+// seg_first[i] = segments of buffers < i; seg_first[n] = total.  One workgroup.
 __global__ __launch_bounds__(1024) void seg_plan_kernel(const uint64_t* __restrict__ len, u32 n, u32 sb,
                                                         u32* __restrict__ seg_first, u32* __restrict__ sflag,
                                                         u32 maxseg, u32* __restrict__ ticket,
-                                                        u32* __restrict__ bclear, u32* __restrict__ seg_buf) {
+                                                        u32* __restrict__ bclear) {
     __shared__ u32 part[1024];
-    __shared__ u32 sf[kPlanLds + 1u];
     const u32 t = threadIdx.x;
     // (fused kernels) every segment's publication flag cleared, the ticket counter at 0, and (the
     // single-pass decode) every buffer's flags
@@ -94,33 +89,11 @@ __global__ __launch_bounds__(1024) void seg_plan_kernel(const uint64_t* __restri
         __syncthreads();
     }
     u32 base = t ? part[t - 1] : 0u;
-    const bool map = seg_buf && n < kPlanLds;
     for (u32 i = b0; i < b1; ++i) {
         seg_first[i] = base;
-        if (map) sf[i] = base;
         base += seg_count(len32(len[i]), sb);
     }
-    if (t == 1023u) {
-        seg_first[n] = part[1023];
-        if (map) sf[n] = part[1023];
-    }
-    if (!map) return;
-    __syncthreads();
-    const u32 total = sf[n] < maxseg ? sf[n] : maxseg;
-    const u32 per2 = (total + 1023u) / 1024u;
-    const u32 g0 = t * per2 < total ? t * per2 : total;
-    const u32 g1 = g0 + per2 < total ? g0 + per2 : total;
-    if (g0 >= g1) return;
-    u32 lo = 0, hi = n;   // the buffer holding g0: sf[lo] <= g0 < sf[lo + 1] (sf strictly increasing)
-    while (hi - lo > 1u) {
-        const u32 mid = (lo + hi) >> 1;
-        if (sf[mid] <= g0) lo = mid;
-        else hi = mid;
-    }
-    for (u32 g = g0; g < g1; ++g) {
-        while (sf[lo + 1u] <= g) ++lo;
-        seg_buf[g] = lo;
-    }
+    if (t == 1023u) seg_first[n] = part[1023];
 }
 
 // the buffer holding global segment g: seg_first[b] <= g < seg_first[b + 1] (every buffer has a
@@ -155,9 +128,6 @@ __global__ __launch_bounds__(kMapBlock) void seg_map_kernel(const u32* __restric
 // [0, seg_count(in_len[0])) (RLE_SEG_ONE).
 #ifndef RLE_SEG_ONE
 #define RLE_SEG_ONE 1
-#endif
-#ifndef RLE_PLAN_MAP   // 1: below kPlanLds buffers the plan kernel writes the segments' buffers (no map launch)
-#define RLE_PLAN_MAP 1
 #endif
 __device__ __forceinline__ u32 seg_total(const u32* seg_first, u32 n, const uint64_t* len, u32 sb) {
     return seg_first ? uniform(seg_first[n]) : seg_count(len32(len[0]), sb);
@@ -1404,7 +1374,7 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
 #if RLE_VARIANTS
     if (seg_res()) {   // (the plan clears the status words: the segments OR into them)
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
-                           maxseg, w.ticket, d_status, nullptr);
+                           maxseg, w.ticket, d_status);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
         hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
@@ -1415,7 +1385,7 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     }
     if (seg_fused()) {   // (the plan clears the status words: the segments OR into them)
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
-                           maxseg, w.ticket, d_status, nullptr);
+                           maxseg, w.ticket, d_status);
         hipLaunchKernelGGL(rle::enc_seg_fused_kernel, dim3(seg_grid(maxseg, ncu)), dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, maxseg, sb, w.summ,
                            w.incl, w.sflag, w.ticket);
@@ -1427,13 +1397,11 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     const bool one = RLE_SEG_ONE && n == 1u;
     uint32_t* const seg_first = one ? nullptr : w.seg_first;
     uint32_t* const seg_buf = one ? nullptr : w.seg_buf;
-    if (!one) {   // (the plan writes the segments' buffers too when it holds seg_first in LDS)
-        const bool pmap = RLE_PLAN_MAP && n < rle::kPlanLds;
-        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr,
-                           maxseg, nullptr, nullptr, pmap ? w.seg_buf : nullptr);
-        if (!pmap)
-            hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
-                               maxseg, w.seg_buf);
+    if (!one) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
+                           nullptr, nullptr);
+        hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
+                           maxseg, w.seg_buf);
     }
     hipLaunchKernelGGL(rle::enc_seg_summary_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, n,
                        seg_first, seg_buf, maxseg, sb, w.summ);
@@ -1463,7 +1431,7 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
 #if RLE_VARIANTS
     if (seg_res()) {
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
-                           maxseg, w.ticket, w.bflag, nullptr);
+                           maxseg, w.ticket, w.bflag);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
         hipLaunchKernelGGL(rle::dec_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
@@ -1479,13 +1447,11 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     const bool one = RLE_SEG_ONE && n == 1u;   // (as in the encode: no plan / map launches for one buffer)
     uint32_t* const seg_first = one ? nullptr : w.seg_first;
     uint32_t* const seg_buf = one ? nullptr : w.seg_buf;
-    if (!one) {   // (the plan writes the segments' buffers too when it holds seg_first in LDS)
-        const bool pmap = RLE_PLAN_MAP && n < rle::kPlanLds;
-        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr,
-                           maxseg, nullptr, nullptr, pmap ? w.seg_buf : nullptr);
-        if (!pmap)
-            hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
-                               maxseg, w.seg_buf);
+    if (!one) {
+        hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, nullptr, 0u,
+                           nullptr, nullptr);
+        hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
+                           maxseg, w.seg_buf);
     }
     hipLaunchKernelGGL(rle::dec_seg_summary_kernel, dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, n,
                        seg_first, seg_buf, maxseg, sb, w.summ);
