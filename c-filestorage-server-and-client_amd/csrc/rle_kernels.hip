@@ -83,7 +83,10 @@ constexpr u32 kEncWaves = RLE_ENC_WAVES;
 #endif
 constexpr u32 kEncSmall = RLE_ENC_SMALL;
 constexpr u32 kEncBlock = kWave * kEncWaves;
-template <u32 kDepth = 2u>
+// kWtMode: the output store policy fixed at compile time (1 write-through, 2 write-back; 0 the launch
+// flag's bit 0 at run time), so that the tile steps carry no branch around each store
+// (RLE_WT_STATIC, round 5)
+template <u32 kDepth = 2u, u32 kWtMode = 0u>
 __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
                                                            const uint64_t* __restrict__ in_len,
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     const u32 U = (u32)U64;
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     const u32x4 rso = make_rsrc(dst, U + U / 2u);
-    EncState st{0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
+    EncState st{0u, 0u, 0u, 0u, 0u, kWtMode ? kWtMode == 1u : (wt & kLaunchWt) != 0u, {}};
     const EncK kc = enc_k();
 #if RLE_STAMPS
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
@@ -368,7 +371,7 @@ __device__ __forceinline__ u32 order_slot_local(u32 s, u32 n) {
 #define RLE_FEW_DEPTH 2
 #endif
 constexpr u32 kFewDepth = RLE_FEW_DEPTH;
-template <u32 kChunks, u32 kDepthT = 0u>
+template <u32 kChunks, u32 kDepthT = 0u, u32 kWtMode = 0u>   // (kWtMode: as encode_kernel's)
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
                                                            const uint64_t* __restrict__ in_len,
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             return;
         }
         const u32x4 rso = make_rsrc(dst, U);
-        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, (wt & kLaunchWt) != 0u, {}};
+        DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, kWtMode ? kWtMode == 1u : (wt & kLaunchWt) != 0u, {}};
         const DecK kc = dec_k();
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
@@ -656,6 +659,9 @@ constexpr uint32_t kFewBuffers = 16;   // launches of up to this many buffers ta
 #define RLE_DEC_CHUNKS_LARGE 96
 #endif
 constexpr uint32_t kDecChunksLarge = RLE_DEC_CHUNKS_LARGE;
+#ifndef RLE_WT_STATIC   // 1: the codec kernels instantiated per store policy (no run-time branch per store)
+#define RLE_WT_STATIC 1
+#endif
 bool dec_order_enabled() {
     static const bool on = !(getenv("RLE_MI355X_DEC_ORDER") && !strcmp(getenv("RLE_MI355X_DEC_ORDER"), "0"));
     return on;
@@ -672,12 +678,13 @@ int encode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
-    auto kern = rle::encode_kernel<2u>;
+    const uint32_t pol = store_policy(n, true);
+    auto kern = !RLE_WT_STATIC ? rle::encode_kernel<2u> : pol ? rle::encode_kernel<2u, 1u> : rle::encode_kernel<2u, 2u>;
     if constexpr (rle::kFewDepth > 2u)
         if (n <= kFewBuffers) kern = rle::encode_kernel<rle::kFewDepth>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n,
-                       store_policy(n, true) | flags);
+                       pol | flags);
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 }  // namespace
@@ -717,13 +724,16 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     }
     // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD);
     // a few buffers (single drop-in calls): the deep tile ring
-    auto kern = n > kDecRound && kDecChunksLarge != rle::kDecChunks ? rle::decode_kernel<kDecChunksLarge>
-                                                                    : rle::decode_kernel<rle::kDecChunks>;
+    const uint32_t pol = store_policy(n, false);
+    const bool large = n > kDecRound && kDecChunksLarge != rle::kDecChunks;
+    auto kern = !RLE_WT_STATIC ? (large ? rle::decode_kernel<kDecChunksLarge> : rle::decode_kernel<rle::kDecChunks>)
+                : large ? (pol ? rle::decode_kernel<kDecChunksLarge, 0u, 1u> : rle::decode_kernel<kDecChunksLarge, 0u, 2u>)
+                        : (pol ? rle::decode_kernel<rle::kDecChunks, 0u, 1u> : rle::decode_kernel<rle::kDecChunks, 0u, 2u>);
     if constexpr (rle::kFewDepth > 2u)
         if (n <= kFewBuffers) kern = rle::decode_kernel<rle::kDecChunks, rle::kFewDepth>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
-                       d_status, n, store_policy(n, false) | flags, (const uint32_t*)order);
+                       d_status, n, pol | flags, (const uint32_t*)order);
     if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
