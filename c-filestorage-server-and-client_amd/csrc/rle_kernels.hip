@@ -229,19 +229,20 @@ __device__ __forceinline__ u32 grouped_add(u32* hist, u32 key, bool on, u32 lane
 // workgroup.
 constexpr u32 kOrderPer = 4;
 constexpr u32 kOrderChunk = 256u * kOrderPer;
-__device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kOrderPer],
-                                            u32 (&rank)[kOrderPer]) {
+template <u32 kPer = kOrderPer>   // buffers per thread (a workgroup's chunk: 256 kPer buffers)
+__device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kPer],
+                                            u32 (&rank)[kPer]) {
     const u32 t = threadIdx.x, lane = t & (kWave - 1);
     for (u32 k = t; k < kOrderBuckets; k += 256u) lh[k] = 0u;
     __syncthreads();
-    const u32 i0 = blockIdx.x * kOrderChunk + t;
+    const u32 i0 = blockIdx.x * (256u * kPer) + t;
 #pragma unroll
-    for (u32 j = 0; j < kOrderPer; ++j) {
+    for (u32 j = 0; j < kPer; ++j) {
         const u32 i = i0 + 256u * j;
         key[j] = i < n ? order_key(in_len[i]) : 0u;
     }
 #pragma unroll
-    for (u32 j = 0; j < kOrderPer; ++j) rank[j] = grouped_add(lh, key[j], i0 + 256u * j < n, lane);
+    for (u32 j = 0; j < kPer; ++j) rank[j] = grouped_add(lh, key[j], i0 + 256u * j < n, lane);
     __syncthreads();
 }
 __global__ __launch_bounds__(256) void dec_order_hist_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
@@ -294,20 +295,24 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
 }
 
 // Issue order in one launch and without global counts (RLE_ORDER_LOCAL, round 5): each workgroup sorts
-// its own kOrderChunk buffers longest first (its LDS histogram, a descending scan of it, each buffer's
-// place = its bucket's start + its rank in the bucket) into order[chunk * kOrderChunk ...], and the
-// decode kernel interleaves the F = n / kOrderChunk full chunks (slot s takes place s / F of chunk
+// its own kLocalChunk buffers longest first (its LDS histogram, a descending scan of it, each buffer's
+// place = its bucket's start + its rank in the bucket) into order[chunk * kLocalChunk ...], and the
+// decode kernel interleaves the F = n / kLocalChunk full chunks (slot s takes place s / F of chunk
 // s % F; the last partial chunk follows them): the i-th heaviest buffers of every chunk are issued
 // together, which on batches whose chunks hold similar mixes (every bench and server batch) is the
 // global longest-first order without the memset, the second launch and the global atomics.
+#ifndef RLE_ORDER_LOCAL_PER   // buffers per thread of the chunk-local sort (chunks of 256 x this)
+#define RLE_ORDER_LOCAL_PER 1
+#endif
+constexpr u32 kLocalPer = RLE_ORDER_LOCAL_PER, kLocalChunk = 256u * kLocalPer;
 __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
                                                               uint32_t* __restrict__ order) {
     __shared__ u32 lh[kOrderBuckets];
     __shared__ u32 wsum[4];
     constexpr u32 kPerT = kOrderBuckets / 256u;
     const u32 t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
-    u32 key[kOrderPer], rank[kOrderPer];
-    order_local(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
+    u32 key[kLocalPer], rank[kLocalPer];
+    order_local<kLocalPer>(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
     // thread t: the 8 buckets from B-1-8t down, in descending bucket order
     u32 c[kPerT], sum = 0u;
 #pragma unroll
@@ -326,11 +331,11 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
         base += c[j];
     }
     __syncthreads();
-    const u32 i0 = blockIdx.x * kOrderChunk + threadIdx.x;
+    const u32 i0 = blockIdx.x * kLocalChunk + threadIdx.x;
 #pragma unroll
-    for (u32 j = 0; j < kOrderPer; ++j) {
+    for (u32 j = 0; j < kLocalPer; ++j) {
         const u32 i = i0 + 256u * j;
-        if (i < n) order[blockIdx.x * kOrderChunk + lh[key[j]] + rank[j]] = i;
+        if (i < n) order[blockIdx.x * kLocalChunk + lh[key[j]] + rank[j]] = i;
     }
 }
 #ifndef RLE_ORDER_LOCAL
@@ -338,9 +343,9 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
 #endif
 // The buffer a decode wave takes at issue slot s of an order made by dec_order_local_kernel.
 __device__ __forceinline__ u32 order_slot_local(u32 s, u32 n) {
-    const u32 F = n / kOrderChunk;   // full chunks, interleaved; the partial one after them
-    if (s >= F * kOrderChunk) return s;
-    return (s % F) * kOrderChunk + s / F;
+    const u32 F = n / kLocalChunk;   // full chunks, interleaved; the partial one after them
+    if (s >= F * kLocalChunk) return s;
+    return (s % F) * kLocalChunk + s / F;
 }
 
 // kChunks: staging chunks per wave (32 B each).  192 hold any tile's output in one pass; the
@@ -712,7 +717,7 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
         order = nullptr;
     }
     if (order && RLE_ORDER_LOCAL) {   // one launch, chunk-local sorts (rle::dec_order_local_kernel)
-        hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kOrderChunk - 1u) / rle::kOrderChunk), dim3(256), 0,
+        hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
                            s, d_in_len, n, order);
     } else if (order) {
         uint32_t* hist = order + n;
