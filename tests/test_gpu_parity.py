@@ -392,9 +392,9 @@ def test_large_batch_decode_plain_stores():
 def test_decode_ragged_batches_past_one_round(n):
     """Batches just past one residency round of the chip (4096 waves): a last round of one to a few
     buffers, XCD-padding workgroups with no buffer, and long / short / serial buffers mixed --
-    each buffer decoded exactly once, bit-exact, every status written.  Up to 16384 buffers the
-    issue order is sorted without a memset (per-workgroup parts), from 16385 with the global
-    histogram (rle_kernels.hip dec_order_*)."""
+    each buffer decoded exactly once, bit-exact, every status written.  The issue order comes from
+    chunk-local sorts of 256 buffers (rle_kernels.hip dec_order_local_kernel), the full chunks
+    interleaved and a partial last chunk (n % 256 buffers: 1, 3, 3, 0, 0, 1 here) after them."""
     rng = np.random.default_rng(n)
     sizes = rng.integers(0, 3000, size=n)
     sizes[::7] = 20000   # a few long buffers, so ranges finish unevenly
