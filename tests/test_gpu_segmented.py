@@ -110,6 +110,29 @@ def test_invalid_streams_take_the_serial_path():
     assert st[0] & R.RLE_STATUS_SERIAL
 
 
+def test_one_buffer_launches():
+    """A segmented launch of ONE buffer takes its segments from its length, without the plan and map
+    launches (rle_segmented.hip RLE_SEG_ONE): every kind at and around segment edges, the empty and
+    one-byte buffers, a stream that declines to the serial path and one that decodes short."""
+    cases = [b"", b"a", bytes(3), O.gen(1, 3, 1000)]
+    for k in (1, 2, 4):
+        for d in (-2, 0, 1, 3):
+            for kind in range(5):
+                cases.append(O.gen(kind, 10 * k + d + kind, k * S + d))
+    for x in cases:
+        _parity([x])
+    good = O.encode(O.gen(2, 5, 2 * S))
+    bad = bytearray(good)
+    pos = S + 50
+    while bad[pos] != bad[pos + 1]:
+        pos += 1
+    bad[pos + 2] = ord(":")
+    for y, U in ((bytes(bad), 2 * S), (good, 2 * S + 9)):
+        dec, st = gpu_decode([y], [U], [U + 16], poison=False, seg=True)
+        ref, _ = O.decode(y, U, U + 16)
+        assert dec[0] == ref
+
+
 def test_dropin_large_files_roundtrip():
     for x in (O.gen(1, 5, 3 << 20), bytes(2 << 20), O.gen(3, 6, (1 << 20) + 1)):
         y = R.compress(x)
