@@ -25,7 +25,7 @@ def main():
     d = sys.argv[1]
     print(f"# Per-kind 64 KiB codec launches ({os.path.basename(d.rstrip('/'))}, rocprofv3 --kernel-trace, median of 5-6 launches)\n")
     print("16384 x 64 KiB per launch (1 GiB of U). Algorithmic bytes = U + C; fraction of 8 TB/s. "
-          "Decode includes neither the issue-order sort's two small launches (listed) nor the memset.\n")
+          "Decode excludes the issue-order sort (its own launch, listed).\n")
     print("| workload | C MB | encode µs | encode frac | decode µs | decode frac | sort µs |")
     print("|---|---|---|---|---|---|---|")
     for wl, kinds in KINDS.items():
