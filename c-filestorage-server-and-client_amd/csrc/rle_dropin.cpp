@@ -148,6 +148,9 @@ size_t g_presize = 1u << 20;   // staging allocated with each thread context (pr
 // instead of hipStreamSynchronize (profiles/r4a_sync_probe.txt: 11.7 against 16.2 us per 4 KiB
 // launch).  RLE_MI355X_POLL=0: synchronize instead.
 bool g_poll = true;
+// How long a completion poll spins (pause) before it yields the core between reads:
+// RLE_MI355X_SPIN_NS (default 50 us, about the longest small call).
+uint64_t g_spin_ns = 50000;
 // Small calls through the resident service (rle_service.h) instead of a launch each:
 // RLE_MI355X_SERVICE=1, in the RLE_VARIANTS test library only (measured slower, round 5).
 bool g_service = false;
@@ -295,6 +298,7 @@ void init_once() {
     if (const char* e = getenv("RLE_MI355X_DEVICE")) g_dev_pin = atoi(e);
     if (const char* e = getenv("RLE_MI355X_SMALL")) g_zerocopy = strcmp(e, "copy") != 0;
     if (const char* e = getenv("RLE_MI355X_POLL")) g_poll = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RLE_MI355X_SPIN_NS")) g_spin_ns = strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_SERVICE")) g_service = strcmp(e, "0") != 0;
     if (const char* e = getenv("RLE_MI355X_ZC_SEG")) g_zc_seg = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_ZC_COOP")) g_zc_coop = strcmp(e, "0") != 0;
@@ -968,7 +972,7 @@ void submit(Ctx* c, Req* r) {
 // so the runtime's record of completed launches stays short.
 constexpr uint32_t kPending = 0xFFFFFFFFu;
 constexpr uint64_t kPollNs = 2000000;
-constexpr uint64_t kSpinNs = 50000;   // then the poll yields the core between reads
+// (g_spin_ns, above: then the poll yields the core between reads)
 constexpr uint32_t kPollSyncEvery = 32;
 uint32_t zc_flags() { return g_poll ? RLE_LAUNCH_STATUS_FLAG : 0u; }
 uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
@@ -989,7 +993,7 @@ uint32_t zc_wait(Ctx* c, const uint64_t* status_word) {
                 const uint64_t t = now_ns();
                 if (!t0) t0 = t;
                 else if (t - t0 > kPollNs) break;
-                else yield = t - t0 > kSpinNs;
+                else yield = t - t0 > g_spin_ns;
             }
             if (yield) sched_yield();   // a long call: leave the core to the server's other threads
             else __builtin_ia32_pause();
@@ -1114,7 +1118,7 @@ uint32_t svc_call(Ctx* c, uint32_t op, uint64_t in_len, uint64_t out_len, uint64
             if (!svc_ensure(c) && __atomic_load_n(&c->svc_h->a.ack, __ATOMIC_ACQUIRE) != seq) return kSvcStopped;
             const uint64_t t = now_ns() - t0;
             if (t > 10000000000ull) die("service request (10 s)", hipErrorUnknown);
-            yield = t > kSpinNs;
+            yield = t > g_spin_ns;
         }
         if (yield) sched_yield();
         else __builtin_ia32_pause();
