@@ -20,10 +20,13 @@ import test_e2e_server as E  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="", help="comma-separated variant names (default: all)")
     a = ap.parse_args()
     variants = (("server_ref", "server_ref", None), ("server_gpu", "server_gpu", None),
                 ("server_gpu_spin0", "server_gpu", {"RLE_MI355X_SPIN_NS": "0"}),
                 ("server_gpu_poll0", "server_gpu", {"RLE_MI355X_POLL": "0"}))
+    if a.only:
+        variants = tuple(v for v in variants if v[0] in a.only.split(","))
     res = {name: {"battery3_cold_s": [], "battery3_warm_s": []} for name, _, _ in variants}
     for r in range(a.reps):
         for name, exe, env in variants:
