@@ -233,14 +233,15 @@ template <u32 kPer = kOrderPer>   // buffers per thread (a workgroup's chunk: 25
 __device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kPer],
                                             u32 (&rank)[kPer]) {
     const u32 t = threadIdx.x, lane = t & (kWave - 1);
+    // the lengths' loads first, so their latency overlaps the histogram's zeroing and barrier
+    const u32 i0 = blockIdx.x * (256u * kPer) + t;
+    uint64_t len[kPer];   // (every lane loads, index clamped: no branch, the wait lands at the first use)
+#pragma unroll
+    for (u32 j = 0; j < kPer; ++j) len[j] = in_len[i0 + 256u * j < n ? i0 + 256u * j : n - 1u];
     for (u32 k = t; k < kOrderBuckets; k += 256u) lh[k] = 0u;
     __syncthreads();
-    const u32 i0 = blockIdx.x * (256u * kPer) + t;
 #pragma unroll
-    for (u32 j = 0; j < kPer; ++j) {
-        const u32 i = i0 + 256u * j;
-        key[j] = i < n ? order_key(in_len[i]) : 0u;
-    }
+    for (u32 j = 0; j < kPer; ++j) key[j] = i0 + 256u * j < n ? order_key(len[j]) : 0u;
 #pragma unroll
     for (u32 j = 0; j < kPer; ++j) rank[j] = grouped_add(lh, key[j], i0 + 256u * j < n, lane);
     __syncthreads();
