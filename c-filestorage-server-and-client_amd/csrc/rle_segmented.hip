@@ -1113,6 +1113,10 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
 // of polls) is only known once its last segment has combined: its segments skip their walks from
 // the first one that knows, the buffer is flagged (bflag, cleared by the plan), and
 // dec_seg_serial_kernel decodes it after this launch, over whatever the earlier segments wrote.
+// kRes false (RLE_MI355X_SEG_RES=2, round 5): the same single pass without the LDS-resident segment
+// (its 28 KB region per workgroup capped it at 3 workgroups per CU): the summary walks the segment
+// through the two DMA slots, and the write walks it again, from the caches if it is still there.
+template <bool kRes>
 __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len,
@@ -1127,7 +1131,8 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
                                                                 u32* __restrict__ sflag, u32* __restrict__ ticket,
                                                                 u32* __restrict__ bflag) {
     constexpr u32 kStage = 32u * kResDecChunks;
-    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kResStride];
+    constexpr u32 kRegion = kRes ? kResStride : 2u * kSlot;   // the resident segment, or two DMA slots
+    __shared__ __attribute__((aligned(16))) uint8_t region_all[kSegWaves * kRegion];
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kSegWaves * kStage];
     __shared__ DecEntry tbl[256];
     __shared__ u32x4 clut[kCompactEntries];   // dec_tile_fast's selectors
@@ -1138,7 +1143,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
         clut[k] = u32x4{kCompactLut.s[4u * k], kCompactLut.s[4u * k + 1u], kCompactLut.s[4u * k + 2u],
                         kCompactLut.s[4u * k + 3u]};
     uint8_t* stage = stage_all + wid * kStage;
-    const uint8_t* region = region_all + wid * kResStride;
+    const uint8_t* region = region_all + wid * kRegion;
     for (u32 k = lane; k < kStage / 16u; k += kWave) reinterpret_cast<u32x4*>(stage)[k] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     u32 total = uniform(seg_first[n]);
@@ -1169,8 +1174,8 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
             seg_range(g - s0, nseg, C, sb, q0, q1);
             uint4 sm = kDecEmpty;
             if (C) {
-                res_load(make_rsrc(src, (C + 15u) & ~15u), q0, ntiles_for(q1 - q0), lane, region);
-                sm = dec_seg_summarize<true>(src, C, q0, q1, lane, region, tbl);
+                if (kRes) res_load(make_rsrc(src, (C + 15u) & ~15u), q0, ntiles_for(q1 - q0), lane, region);
+                sm = dec_seg_summarize<kRes>(src, C, q0, q1, lane, region, tbl);
             }
             if (lane == 0) publish(summ + g, sm, sflag + g, kFlagAgg);
             bool late = false;
@@ -1198,7 +1203,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
                 if ((last && c.serial) || late) atomicOr(bflag + b, kFlagSerial);
             }
             if (!c.serial)
-                dec_seg_write<true, kResDecChunks>(src, dst, C, U, q0, q1, uniform(mine.x), uniform(mine.y), last, lane,
+                dec_seg_write<kRes, kResDecChunks>(src, dst, C, U, q0, q1, uniform(mine.x), uniform(mine.y), last, lane,
                                                    region, stage, tbl, clut, status ? status + b : nullptr);
         }
     }
@@ -1306,14 +1311,16 @@ int device_cus(int* ncu) {
 #ifndef RLE_SEG_RES_DEFAULT
 #define RLE_SEG_RES_DEFAULT 0
 #endif
-bool seg_res() {
-    if (!RLE_VARIANTS) return false;   // (product build: RLE_MI355X_SEG_RES is not read)
-    static const bool on = [] {
+// 0 off, 1 the resident single pass, 2 the single pass without the resident segment (decode)
+int seg_res_mode() {
+    if (!RLE_VARIANTS) return 0;   // (product build: RLE_MI355X_SEG_RES is not read)
+    static const int m = [] {
         const char* e = getenv("RLE_MI355X_SEG_RES");
-        return e ? e[0] != '0' : RLE_SEG_RES_DEFAULT != 0;
+        return e ? atoi(e) : RLE_SEG_RES_DEFAULT;
     }();
-    return on;
+    return m;
 }
+bool seg_res() { return seg_res_mode() == 1; }
 inline uint32_t seg_bytes(uint64_t total, int ncu) {
     if (seg_res()) return (rle::kResTiles - 1u) * rle::kTileStep;
     if (RLE_SEG_TILES_FIX) return (uint32_t)RLE_SEG_TILES_FIX * rle::kTileStep;
@@ -1429,12 +1436,13 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     const uint8_t* in = (const uint8_t*)d_in;
     uint8_t* out = (uint8_t*)d_out;
 #if RLE_VARIANTS
-    if (seg_res()) {
+    if (seg_res_mode() == 1 || seg_res_mode() == 2) {
         hipLaunchKernelGGL(rle::seg_plan_kernel, dim3(1), dim3(1024), 0, s, d_in_len, n, sb, w.seg_first, w.sflag,
                            maxseg, w.ticket, w.bflag);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
-        hipLaunchKernelGGL(rle::dec_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
+        hipLaunchKernelGGL(seg_res_mode() == 1 ? rle::dec_seg_res_kernel<true> : rle::dec_seg_res_kernel<false>,
+                           dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
                            dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first,
                            w.seg_buf, maxseg, sb, w.summ, w.incl, w.sflag, w.ticket, w.bflag);
