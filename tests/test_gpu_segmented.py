@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 # 7056 (7 tiles) for the resident single-pass kernels (RLE_MI355X_SEG_RES=1, which
 # test_resident_single_pass below sets for a second run of this module)
 RES = os.environ.get("RLE_MI355X_SEG_RES", "0") == "1"
+RES_MODE = os.environ.get("RLE_MI355X_SEG_RES", "0")   # "2": the single pass without the resident segment
 S = 7056 if RES else 64512
 
 
@@ -190,16 +191,18 @@ def test_fused_single_pass_encode():
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
 
 
-def test_resident_single_pass():
-    """The resident single-pass segmented kernels (RLE_MI355X_SEG_RES=1, read at load: a fresh
-    process): this whole module again, with its segment edges at the resident segment length, plus
-    the drop-in's large files, against the oracle."""
-    if RES:
-        pytest.skip("already the resident run")
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_resident_single_pass(mode):
+    """The single-pass segmented kernels (read at load: a fresh process): RLE_MI355X_SEG_RES=1, the
+    resident form (encode and decode; the segment edges at its segment length), and =2, the decode
+    without the resident segment (round 5: its write walk re-reads the segment): this whole module
+    again, plus the drop-in's large files, against the oracle."""
+    if RES_MODE != "0":
+        pytest.skip("already a single-pass run")
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, RLE_MI355X_SEG_RES="1", RLE_MI355X_LIB=_variants_lib(os.path.dirname(here)))
+    env = dict(os.environ, RLE_MI355X_SEG_RES=mode, RLE_MI355X_LIB=_variants_lib(os.path.dirname(here)))
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
                         os.path.join(here, "test_gpu_segmented.py"), "-k", "not fused and not resident"],
                        env=env, capture_output=True, text=True, timeout=300)
