@@ -741,13 +741,21 @@ def north_star(args, stream, dev):
     te = time_kernels(lambda: N.encode(stream), 20, stream)
     nok = bool(torch.equal(N.d_out, N.d_in))
     nalg = N.u_bytes + nc
+    # the same memory traffic without the token work: one wave per buffer streaming its C bytes in
+    # decode tiles and writing its U bytes, the decode's occupancy and issue order (overwrites d_out)
+    tp = time_kernels(lambda: R.decode_pattern(N.d_c, N.coffs, N.clen, N.d_out, N.offs, N.lens, stream), 20, stream)
     ncopy = copy_ceiling(N, nalg, 20, stream)
     north = {"workload": WORKLOADS["dec64k"]["desc"], "decode_us": td * 1e6,
              "decode_U_GiBps": N.u_bytes / td / GIB, "encode_U_GiBps": N.u_bytes / te / GIB,
              "decode_GBps": nalg / td / 1e9, "decode_frac": round(nalg / td / 1e9 / HBM_PEAK_GBPS, 4),
              "decode_frac_of_copy": round(ncopy["us"] / (td * 1e6), 4),
              "encode_GBps": nalg / te / 1e9, "u_bytes": N.u_bytes, "c_bytes": nc, "verified": nok,
-             "copy_ceiling": ncopy}
+             "copy_ceiling": ncopy,
+             "pattern_ceiling": {"us": round(tp * 1e6, 3), "GBps": round(nalg / tp / 1e9, 2),
+                                 "frac": round(nalg / tp / 1e9 / HBM_PEAK_GBPS, 4),
+                                 "op": "rle_decode_pattern_device: the decode's tile reads and output writes, "
+                                       "one wave per buffer, its occupancy and issue order, no token work"},
+             "decode_frac_of_pattern": round(tp / td, 4)}
     del N
     torch.cuda.empty_cache()
     return north

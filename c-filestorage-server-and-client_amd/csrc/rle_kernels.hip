@@ -348,6 +348,27 @@ __device__ __forceinline__ u32 order_slot_local(u32 s, u32 n) {
     if (s >= F * kLocalChunk) return s;
     return (s % F) * kLocalChunk + s / F;
 }
+#ifndef RLE_ORDER_XCD   // 1: each XCD interleaves only the chunks of its own contiguous slice
+#define RLE_ORDER_XCD 0
+#endif
+// The place in order[] that workgroup wg's wave wid takes (n: none) with RLE_ORDER_XCD: XCD x =
+// wg % 8 owns places [x R, x R + L) (R = its slots, L clipped at n), as xcd_buffer gives it buffers;
+// its k-th slot takes place k / F of its k % F-th full chunk (F of them inside the slice), then the
+// slice's head and tail fragments in index order.  Each XCD walks its own slice longest first, so
+// the waves in flight on one XCD stay within an eighth of the batch instead of all of it.
+__device__ __forceinline__ u32 order_place_xcd(u32 wg, u32 ngrid, u32 wid, u32 n) {
+    const u32 R = ngrid / kXcds * kDecWaves;   // launcher makes ngrid a multiple of 8
+    const u32 a = (wg % kXcds) * R;
+    const u32 k = (wg / kXcds) * kDecWaves + wid;
+    if (a >= n || k >= n - a) return n;
+    const u32 L = n - a < R ? n - a : R;
+    const u32 c0 = (a + kLocalChunk - 1u) / kLocalChunk, c1 = (a + L) / kLocalChunk;
+    const u32 F = c1 > c0 ? c1 - c0 : 0u;
+    if (k < F * kLocalChunk) return (c0 + k % F) * kLocalChunk + k / F;
+    if (F == 0u) return a + k;
+    const u32 r = k - F * kLocalChunk, h = c0 * kLocalChunk - a;
+    return r < h ? a + r : c1 * kLocalChunk + (r - h);
+}
 
 // kChunks: staging chunks per wave (32 B each).  192 hold any tile's output in one pass; the
 // launcher takes 96 (3 KiB per wave: 7 workgroups per CU instead of 4) for batches past one
@@ -408,14 +429,16 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
 #endif
     if (order && RLE_ORDER_MODE != 3) {
         u32 slot = blockIdx.x * kDecWaves + wid;
-        if (RLE_ORDER_MODE == 1 && (gridDim.x & 7u) == 0u) {
+        if (RLE_ORDER_XCD && RLE_ORDER_LOCAL && RLE_ORDER_MODE == 0) {
+            slot = uniform(order_place_xcd(blockIdx.x, gridDim.x, wid, n));
+        } else if (RLE_ORDER_MODE == 1 && (gridDim.x & 7u) == 0u) {
             const u32 nb = gridDim.x >> 3, h = blockIdx.x >> 3;
             const u32 ph = (h & 1u) ? nb - 1u - (h >> 1) : (h >> 1);
             slot = (8u * ph + (blockIdx.x & 7u)) * kDecWaves + wid;
         } else if (RLE_ORDER_MODE == 2 && slot < n) {
             slot = (slot & 1u) ? n - 1u - (slot >> 1) : (slot >> 1);
         }
-        if (RLE_ORDER_LOCAL && slot < n) slot = uniform(order_slot_local(slot, n));
+        if (!(RLE_ORDER_XCD && RLE_ORDER_MODE == 0) && RLE_ORDER_LOCAL && slot < n) slot = uniform(order_slot_local(slot, n));
         b = slot < n ? uniform(order[slot]) : n;
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
@@ -561,6 +584,59 @@ __global__ void gen_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict
         }
     }
     for (uint64_t q = U & ~3ull; q < U; ++q) p[q] = (uint8_t)(acc >> (8u * (uint32_t)(q & 3u)));
+}
+
+// ================================================================ the decode's memory pattern (measurement only)
+// bench.py's second north-star ceiling: the large-batch decode's memory traffic without its token
+// work.  Each wave streams its buffer's C bytes in through decode_kernel's tile walk (1 KiB LDS-DMA
+// tiles, two in flight, walk_tiles) and writes its U bytes out in 16-byte-per-lane stores, each tile
+// taking its share of the output; workgroups, LDS (7 per CU) and the issue order as decode_kernel<96>.
+// Not the codec: the output bytes are the tiles' bytes repeated.
+constexpr u32 kPatternPad = kDecWaves * 32u * 96u + (u32)sizeof(DecTable) + kCompactEntries * 16u;
+__global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __restrict__ in,
+                                                            const uint64_t* __restrict__ in_off,
+                                                            const uint64_t* __restrict__ in_len,
+                                                            uint8_t* __restrict__ out,
+                                                            const uint64_t* __restrict__ out_off,
+                                                            const uint64_t* __restrict__ out_len, uint32_t n,
+                                                            const uint32_t* __restrict__ order) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * 2u * kSlot];
+    __shared__ uint8_t pad[kPatternPad];   // decode_kernel<96>'s staging, table and selectors: its occupancy
+    const u32 lane = threadIdx.x & (kWave - 1);
+    const u32 wid = uniform(threadIdx.x / kWave);
+    if (threadIdx.x == 0) ((volatile uint8_t*)pad)[blockIdx.x % kPatternPad] = 0;
+    u32 b;
+    if (order) {
+        const u32 slot = blockIdx.x * kDecWaves + wid;
+        const u32 place = RLE_ORDER_XCD ? order_place_xcd(blockIdx.x, gridDim.x, wid, n)
+                                        : slot < n ? order_slot_local(slot, n) : n;
+        b = place < n ? uniform(order[uniform(place)]) : n;
+    } else {
+        b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
+    }
+    b = uniform(b);
+    if (b >= n) return;
+    auto u64 = [](uint64_t x) { return (uint64_t)uniform((u32)x) | ((uint64_t)uniform((u32)(x >> 32)) << 32); };
+    const uint64_t C64 = u64(in_len[b]), U64 = u64(out_len[b]);
+    if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) return;
+    const u32 C = (u32)C64, U = (u32)U64;
+    const uint8_t* src = in + u64(in_off[b]);
+    uint8_t* dst = out + u64(out_off[b]);
+    if (((uintptr_t)src | (uintptr_t)dst) & 15u) return;
+    const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
+    const u32x4 rso = make_rsrc(dst, U);
+    const uint8_t* slots = slots_all + wid * 2u * kSlot;
+    const u32 ntiles = ntiles_for(C);
+    u32 written = 0;
+    walk_tiles(rsi, 0u, ntiles, lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
+        nx();
+        const u32 upto = t + 1u == ntiles ? U : (u32)(((uint64_t)(t + 1u) * U / ntiles) & ~15ull);
+        u32 k = 0;
+        for (u32 o = written; o < upto; o += 16u * kWave, ++k) vstore(rso, o + 16u * lane < upto ? o + 16u * lane : kOOB, v, false);
+        written = upto;
+        return k;
+    });
 }
 
 // ================================================================ streaming copy (measurement only)
@@ -810,6 +886,27 @@ extern "C" int rle_gen_synthetic_device(void* d_out, const uint64_t* d_off, cons
     if (!d_out || !d_off || !d_len) return RLE_E_INVAL;
     hipLaunchKernelGGL(rle::gen_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (uint8_t*)d_out,
                        d_off, d_len, d_kind, d_index, n);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
+
+extern "C" int rle_decode_pattern_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                         void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len, uint32_t n,
+                                         void* stream) {
+    if (n == 0) return RLE_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len || n > kMaxGrid) return RLE_E_INVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    uint32_t* order = nullptr;   // the decode's issue order (decode_launch)
+    if (n > kDecRound && dec_order_enabled() && hipMallocAsync((void**)&order, sizeof(uint32_t) * (size_t)n, s) != hipSuccess) {
+        (void)hipGetLastError();
+        order = nullptr;
+    }
+    if (order)
+        hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
+                           s, d_in_len, n, order);
+    hipLaunchKernelGGL(rle::pattern_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
+                       (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, n,
+                       (const uint32_t*)order);
+    if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 

@@ -104,6 +104,8 @@ def lib():
     L.rle_mi355x_set_coop_mode.argtypes = [ctypes.c_int]
     L.rle_copy_device.restype = ctypes.c_int
     L.rle_copy_device.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    L.rle_decode_pattern_device.restype = ctypes.c_int
+    L.rle_decode_pattern_device.argtypes = [vp] * 6 + [ctypes.c_uint32, vp]
     for f, a in (("rle_dist_available", [ctypes.c_char_p]),
                  ("rle_dist_unique_id", [vp, sz, ctypes.c_char_p]),
                  ("rle_dist_init", [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
@@ -317,6 +319,16 @@ def copy_device(dst, src, nbytes, stream=None):
     rc = lib().rle_copy_device(_ptr(dst), _ptr(src), int(nbytes), _stream_ptr(stream))
     if rc != RLE_OK:
         raise RLEError(f"rle_copy_device failed: {rc}")
+
+
+def decode_pattern(d_in, in_offs, in_lens, d_out, out_offs, out_lens, stream=None):
+    """rle_decode_pattern_device: the large-batch decode's memory traffic (tiles of C in, U out, one
+    wave per buffer, the decode's occupancy and issue order) without its token work; bench.py times
+    it as the ceiling of that access pattern.  Not a decode: d_out receives the tiles' bytes."""
+    rc = lib().rle_decode_pattern_device(_ptr(d_in), _ptr(in_offs), _ptr(in_lens), _ptr(d_out), _ptr(out_offs),
+                                         _ptr(out_lens), in_offs.numel(), _stream_ptr(stream))
+    if rc != RLE_OK:
+        raise RLEError(f"rle_decode_pattern_device failed: {rc}")
 
 
 def set_coop_mode(mode: int):

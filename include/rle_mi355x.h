@@ -215,6 +215,13 @@ int rle_mi355x_set_coop_mode(int mode);
  * times it as the practical HBM ceiling of SURVEY.md §8(d).  RLE_E_INVAL on bad sizes. */
 int rle_copy_device(void* d_dst, const void* d_src, uint64_t nbytes, void* stream);
 
+/* Measurement only (not the codec): the large-batch decode's memory traffic without its token work:
+ * each of the n buffers (decode_batch arguments) read in decode tiles and U bytes written, one wave
+ * per buffer, the decode's occupancy and issue order.  bench.py times it beside the north-star decode
+ * as the ceiling of that access pattern.  The output bytes are not a decode. */
+int rle_decode_pattern_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
+                              const uint64_t* d_out_off, const uint64_t* d_out_len, uint32_t n, void* stream);
+
 /* The drop-in's background start-up (HIP runtime, warm thread contexts) at library load: 1 when this
  * process started it, 0 otherwise.  It starts in a program that links the library (the reference
  * server, INTEGRATION.md §2: the library is among the main program's DT_NEEDED entries) or whenever
