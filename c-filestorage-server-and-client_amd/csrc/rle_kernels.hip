@@ -5,6 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 namespace rle {
 
 #ifndef RLE_XCD_MAP
@@ -749,6 +751,81 @@ bool dec_order_enabled() {
     return on;
 }
 
+#ifndef RLE_ORDER_CACHE   // 1: per-(device, stream) cached issue-order arrays
+#define RLE_ORDER_CACHE 1
+#endif
+// The issue order's device array.  A hipFreeAsync + hipMallocAsync pair per launch left a 5.8 us gap
+// on the queue between back-to-back large decodes (profiles/r5an_order_gap.md); instead each
+// (device, stream) keeps a grow-only array (kOrderStreams of them; more streams, and launches being
+// captured into a graph, take the per-launch pair).  The lock is held until the order and decode
+// kernels are both enqueued, so host threads sharing a stream cannot interleave their launches.
+struct OrderArray {
+    uint32_t* p = nullptr;
+    hipStream_t s = nullptr;
+    bool pooled = false;   // a per-launch array: freed on the stream after the decode
+    std::unique_lock<std::mutex> lk;
+    ~OrderArray() {   // early returns (order_release clears p)
+        if (pooled && p) (void)hipFreeAsync(p, s);
+    }
+};
+constexpr uint32_t kOrderStreams = 16;
+struct OrderSlot {
+    int dev;
+    hipStream_t s;
+    uint32_t* p;
+    size_t cap;
+};
+std::mutex g_order_mu;
+OrderSlot g_order_slots[kOrderStreams];
+uint32_t g_order_count = 0;
+void order_acquire(OrderArray& o, hipStream_t s, size_t bytes) {
+    o.s = s;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
+    int dev = -1;
+    if (RLE_ORDER_CACHE && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
+        hipGetDevice(&dev) == hipSuccess) {
+        o.lk = std::unique_lock<std::mutex>(g_order_mu);
+        OrderSlot* e = nullptr;
+        for (uint32_t i = 0; i < g_order_count && !e; ++i)
+            if (g_order_slots[i].s == s && g_order_slots[i].dev == dev) e = &g_order_slots[i];
+        if (!e && g_order_count < kOrderStreams) {
+            e = &g_order_slots[g_order_count++];
+            *e = OrderSlot{dev, s, nullptr, 0};
+        }
+        if (e && e->cap < bytes) {   // grow: the old array is freed behind this stream's earlier decodes
+            const size_t cap = bytes > (1u << 20) ? bytes : (1u << 20);
+            uint32_t* q = nullptr;
+            if (hipMallocAsync((void**)&q, cap, s) == hipSuccess) {
+                if (e->p) (void)hipFreeAsync(e->p, s);
+                e->p = q;
+                e->cap = cap;
+            } else {
+                (void)hipGetLastError();
+                e = nullptr;
+            }
+        }
+        if (e) {
+            o.p = e->p;
+            return;
+        }
+        o.lk.unlock();
+    }
+    (void)hipGetLastError();
+    if (hipMallocAsync((void**)&o.p, bytes, s) != hipSuccess) {
+        (void)hipGetLastError();
+        o.p = nullptr;
+        return;
+    }
+    o.pooled = true;
+}
+// After the decode's launch: frees a per-launch array on the stream (RLE_E_HIP when that fails).
+bool order_release(OrderArray& o) {
+    const bool ok = !(o.pooled && o.p && hipFreeAsync(o.p, o.s) != hipSuccess);
+    o.p = nullptr;
+    if (o.lk.owns_lock()) o.lk.unlock();
+    return ok;
+}
+
 }  // namespace
 
 extern "C" size_t rle_max_compressed_size(size_t U) { return U + U / 2; }
@@ -786,13 +863,10 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     if (n > kMaxGrid) return RLE_E_INVAL;
     const hipStream_t s = (hipStream_t)stream;
     // more buffers than one residency round: issue them longest first (rle::dec_order_kernel)
-    uint32_t* order = nullptr;   // [n] issue order, then [kOrderBuckets] counts and cursors
     constexpr size_t kOrderExtra = RLE_ORDER_LOCAL ? 0u : 2u * rle::kOrderBuckets;
-    if (n > kDecRound && dec_order_enabled() &&
-        hipMallocAsync((void**)&order, sizeof(uint32_t) * ((size_t)n + kOrderExtra), s) != hipSuccess) {
-        (void)hipGetLastError();
-        order = nullptr;
-    }
+    OrderArray oa;   // [n] issue order, then [kOrderBuckets] counts and cursors
+    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, sizeof(uint32_t) * ((size_t)n + kOrderExtra));
+    uint32_t* order = oa.p;
     if (order && RLE_ORDER_LOCAL) {   // one launch, chunk-local sorts (rle::dec_order_local_kernel)
         hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
                            s, d_in_len, n, order);
@@ -816,7 +890,7 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
                        d_status, n, pol | flags, (const uint32_t*)order);
-    if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;
+    if (!order_release(oa)) return RLE_E_HIP;
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 }  // namespace
@@ -895,18 +969,16 @@ extern "C" int rle_decode_pattern_device(const void* d_in, const uint64_t* d_in_
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len || n > kMaxGrid) return RLE_E_INVAL;
     const hipStream_t s = (hipStream_t)stream;
-    uint32_t* order = nullptr;   // the decode's issue order (decode_launch)
-    if (n > kDecRound && dec_order_enabled() && hipMallocAsync((void**)&order, sizeof(uint32_t) * (size_t)n, s) != hipSuccess) {
-        (void)hipGetLastError();
-        order = nullptr;
-    }
+    OrderArray oa;   // the decode's issue order (decode_launch)
+    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, sizeof(uint32_t) * (size_t)n);
+    uint32_t* order = oa.p;
     if (order)
         hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
                            s, d_in_len, n, order);
     hipLaunchKernelGGL(rle::pattern_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, n,
                        (const uint32_t*)order);
-    if (order && hipFreeAsync(order, s) != hipSuccess) return RLE_E_HIP;
+    if (!order_release(oa)) return RLE_E_HIP;
     return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
 }
 

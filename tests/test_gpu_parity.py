@@ -412,6 +412,56 @@ def test_decode_ragged_batches_past_one_round(n):
     assert all(st[i] & ~R.RLE_STATUS_SHORT == 0 for i in range(n) if (i - 3) % 1001)
 
 
+def test_large_decodes_from_threads_and_streams():
+    """Large decodes (past one residency round, so each takes an issue-order array) launched by four
+    host threads: two on their own streams, two sharing one stream, several times each, with
+    growing batch sizes (the per-stream order arrays grow, rle_kernels.hip order_acquire).  Every
+    output bit-exact.  The order and decode launches of one call must not interleave with another
+    thread's on the shared stream."""
+    rng = np.random.default_rng(33)
+    n = 9000
+    xs = [O.gen(i % 5, 3 * i + 2, int(rng.integers(0, 1500))) for i in range(n)]
+    ys = [O.encode(x) for x in xs]
+    in_offs, in_total = R.layout([len(y) for y in ys])
+    host = np.zeros(in_total, np.uint8)
+    for y, o in zip(ys, in_offs):
+        host[o:o + len(y)] = np.frombuffer(y, np.uint8)
+    d_c = torch.from_numpy(host).to(DEV)
+    sizes = [len(x) for x in xs]
+    out_offs, out_total = R.layout(sizes)
+    want = np.full(out_total, POISON, np.uint8)   # the slots' alignment padding stays poisoned
+    for x, o in zip(xs, out_offs):
+        want[o:o + len(x)] = np.frombuffer(x, np.uint8)
+    coffs, clens, uoffs, ulens = _i64(in_offs), _i64([len(y) for y in ys]), _i64(out_offs), _i64(sizes)
+    shared = torch.cuda.Stream(DEV)
+    streams = [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV), shared, shared]
+    outs = [torch.full((out_total + 16,), POISON, dtype=torch.uint8, device=DEV) for _ in streams]
+    stats = [torch.full((n,), 0x7777, dtype=torch.int32, device=DEV) for _ in streams]
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(k):
+        try:
+            for m in (4100, 6000, n, n, 5000):   # prefixes: the order arrays grow, then are reused
+                with torch.cuda.stream(streams[k]):
+                    R.decode_batch(d_c, coffs[:m], clens[:m], outs[k], uoffs[:m], ulens[:m], None, stats[k][:m],
+                                   stream=streams[k])
+        except Exception as e:   # noqa: BLE001 (reported below)
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(len(streams))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(len(streams)):
+        got = outs[k].cpu().numpy()[:out_total]
+        assert np.array_equal(got, want), f"thread {k}: decoded bytes differ"
+        assert int(stats[k].abs().sum().item()) == 0
+
+
 @pytest.mark.parametrize("seg", [False, True])
 def test_uniform_tiles(seg):
     """Long runs ("v v 9" tokens over whole tiles: the uniform-tile path of rle_device.h
