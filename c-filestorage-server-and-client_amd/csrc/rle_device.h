@@ -1320,6 +1320,8 @@ struct DecState {
     u32 vrun = 0;       // RLE_DEC_VRUN: 0x100 | v while the staged partial chunk is all v and staging
                         // chunk 1 holds exactly one key, kv at position 0 (after a single-value tile)
     bool sv = false;    // the last tile was single-value (dec_fill_run): the next tries the uniform test
+    bool hold_ok = false;   // RLE_DEC_HOLD in this kernel (the one-wave decode only)
+    u32 vhold = 0;          // chunks of st.fillc after `flushed` held back to a 128-byte line (dec_release)
 };
 
 // Bank spread of the decode staging (RLE_SWZ).  Unswizzled, a random-data tile decodes 16 positions
@@ -1881,16 +1883,43 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
 
 // Single-value tile (dec_tile): ttot copies of v after the staged partial chunk.  The caller sets
 // the tile's exit state (st.d, st.prev).
+#ifndef RLE_DEC_ALIGN   // 1: single-value tiles' stores start on 128-byte lines (dec_fill_run)
+#define RLE_DEC_ALIGN 0
+#endif
 #ifndef RLE_DEC_VRUN   // 1: consecutive single-value tiles of one byte skip the staging (st.vrun)
 #define RLE_DEC_VRUN 1
 #endif
+#ifndef RLE_DEC_HOLD   // 1: single-value tiles store up to a 128-byte line and hold back the rest (st.vhold)
+#define RLE_DEC_HOLD 0
+#endif
+// Store the chunks a single-value tile held back (st.vhold of them, all st.fillc), before any path
+// that stages from `flushed`.  Held chunks exist only while st.vrun says the staged partial chunk is
+// all st.fillc too, so afterwards staging chunk 1 is that partial chunk again.  Returns the store
+// instructions issued (0 or 1).
+__device__ __forceinline__ u32 dec_release(u32 lane, u32x4 rso, DecState& st) {
+    if (!RLE_DEC_HOLD || st.vhold == 0u) return 0u;
+    const u32 vv = rep4(st.fillc);
+    vstore(rso, lane < st.vhold ? st.flushed + 16u * lane : kOOB, u32x4{vv, vv, vv, vv}, st.wt);
+    st.flushed += 16u * st.vhold;
+    st.vhold = 0u;
+    return 1u;
+}
 __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st) {
-    const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl = total >> 4;
-    const u32 vv = rep4(v);
     // the previous tile was single-value tile of the same byte that left staging chunk 1 as one key
     // kv at position 0: the staged positions are all v, so chunk 0 is rep4(v) without reading or
     // filling the staging, and the staging stays as it is when this tile leaves a partial chunk too
+    // (held-back chunks, st.vhold, are all v as well and are simply stored with this tile's)
     const bool known = RLE_DEC_VRUN && st.vrun == (0x100u | v);
+    const u32 pre = known ? 0u : dec_release(lane, rso, st);
+    const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl_all = total >> 4;
+    const u32 vv = rep4(v);
+    // RLE_DEC_HOLD: when this tile leaves a partial chunk of v (the state stays known), store only up
+    // to the last 128-byte line boundary: the next tile's stores then start on a line, so no line is
+    // written in two halves by two tiles (the pattern kernel: -3 %, profiles/r5ap_*)
+    const u32 hold = RLE_DEC_HOLD && st.hold_ok && RLE_DEC_VRUN && nfl_all != 0u && (total & 15u) != 0u
+                         ? ((rso.x >> 4) + (st.flushed >> 4) + nfl_all) & 7u : 0u;
+    const u32 nfl = nfl_all - (known || hold < nfl_all ? hold : 0u);   // (unknown: chunk 0 mixes staged keys)
+    const u32 held = nfl_all - nfl;
     u32 c0[4] = {vv, vv, vv, vv};
     if (!known) {
         // chunk 0: the staged positions [0, rel0) filled like a flush, then v (every lane computes it)
@@ -1907,19 +1936,23 @@ __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* 
             c0[k] = (fv[k] & m) | (vv & ~m);
         }
     }
-    const u32 rounds = (nfl + kWave - 1u) / kWave;
+    // RLE_DEC_ALIGN: lane l of store k takes chunk 64 k + l - r, r = the chunks between the last
+    // 128-byte line start and the first store address, so every store instruction covers whole
+    // lines (8 for 64 lanes, not 9); an extra store when nfl + r passes a multiple of 64
+    const u32 r = RLE_DEC_ALIGN ? ((rso.x >> 4) + (st.flushed >> 4)) & 7u : 0u;
+    const u32 rounds = (nfl + r + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
-        const u32 c = k * kWave + lane;
+        const u32 c = k * kWave + lane - r;   // (wraps past nfl for the r lanes before chunk 0)
         const u32x4 o = c == 0u ? u32x4{c0[0], c0[1], c0[2], c0[3]} : u32x4{vv, vv, vv, vv};
         vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, o, st.wt);
     }
-    if (!(known && nfl != 0u && (total & 15u) != 0u)) {
+    if (!(known && nfl_all != 0u && (total & 15u) != 0u)) {
         wave_lds_sync();   // every lane has read staging chunk 1
         // staging chunk 1 = the new partial chunk: the old keys plus a key at rel0 (nothing flushed),
         // else a key at position 0 (when anything is left) and zeros
         const u32 kv = kKeyFlag | v;
         if (lane == 0u) {
-            if (nfl == 0u) {
+            if (nfl_all == 0u) {
                 *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(lds_addr(stage) + 32u + 2u * rel0)) = (uint16_t)kv;
             } else {
                 const u32 k0 = (total & 15u) ? kv : 0u;
@@ -1929,12 +1962,13 @@ __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* 
         }
         wave_lds_sync();
     }
-    st.vrun = (nfl != 0u && (total & 15u) != 0u) ? (0x100u | v) : 0u;
+    st.vrun = (nfl_all != 0u && (total & 15u) != 0u) ? (0x100u | v) : 0u;
     st.sv = true;
     st.fillc = v;
     st.flushed += 16u * nfl;
+    st.vhold = held;
     st.out_pos += ttot;
-    return rounds;
+    return rounds + pre;
 }
 __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st,
                                              const DecPrep& pr) {
@@ -1987,9 +2021,21 @@ __device__ __forceinline__ bool dec_uniform_tile(const u32x4 cur, u32 lane, u32 
 // One tile from its preparation (dec_prepare): returns the store instructions issued, or ~0u (the
 // stream needs the exact serial path).
 template <bool kFast = false, u32 kChunks = kDecChunks>
+__device__ __forceinline__ u32 dec_tile_pr_body(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
+                                                uint8_t* stage, uint8_t* dst, u32x4 rso, DecState& st, const DecK& kc,
+                                                const u32x4* clut);
+template <bool kFast = false, u32 kChunks = kDecChunks>
 __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
                                            uint8_t* stage, uint8_t* dst, u32x4 rso, DecState& st, const DecK& kc,
                                            const u32x4* clut) {
+    const u32 rel = dec_release(lane, rso, st);   // (RLE_DEC_HOLD: every path below stages from `flushed`)
+    const u32 r = dec_tile_pr_body<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
+    return r == ~0u ? r : r + rel;
+}
+template <bool kFast, u32 kChunks>
+__device__ __forceinline__ u32 dec_tile_pr_body(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
+                                                uint8_t* stage, uint8_t* dst, u32x4 rso, DecState& st, const DecK& kc,
+                                                const u32x4* clut) {
     // Segments (Co < C; rle_segmented.hip) end on tile edges, so their last tile (a tail tile) is a
     // whole tile whose tail form clips its stores at its output end: the next segment's output is
     // another wave's.  A segment's first tile takes the literal path when nothing is staged yet (its

@@ -505,6 +505,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         }
         const u32x4 rso = make_rsrc(dst, U);
         DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, kWtMode ? kWtMode == 1u : (wt & kLaunchWt) != 0u, {}};
+        st.hold_ok = true;
         const DecK kc = dec_k();
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
@@ -531,6 +532,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         u32 stat = RLE_STATUS_OK;
         if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage, kStageB);
         else {
+            dec_release(lane, rso, st);
             dec_finish(st, U, lane, stage, rso, dst);
             stat = dec_tiled_status(st, U);
         }
@@ -594,6 +596,12 @@ __global__ void gen_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict
 // tiles, two in flight, walk_tiles) and writes its U bytes out in 16-byte-per-lane stores, each tile
 // taking its share of the output; workgroups, LDS (7 per CU) and the issue order as decode_kernel<96>.
 // Not the codec: the output bytes are the tiles' bytes repeated.
+#ifndef RLE_PATTERN_SHIFT   // experiments: stores line-aligned by shifting lanes (tile shares unchanged)
+#define RLE_PATTERN_SHIFT 0
+#endif
+#ifndef RLE_PATTERN_ALIGN   // experiments: each tile's output share ends on a multiple of this (16: the decode's stores)
+#define RLE_PATTERN_ALIGN 16
+#endif
 constexpr u32 kPatternPad = kDecWaves * 32u * 96u + (u32)sizeof(DecTable) + kCompactEntries * 16u;
 __global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __restrict__ in,
                                                             const uint64_t* __restrict__ in_off,
@@ -633,9 +641,15 @@ __global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __res
     walk_tiles(rsi, 0u, ntiles, lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
         nx();
-        const u32 upto = t + 1u == ntiles ? U : (u32)(((uint64_t)(t + 1u) * U / ntiles) & ~15ull);
+        const u32 upto = t + 1u == ntiles ? U : (u32)(((uint64_t)(t + 1u) * U / ntiles) & ~(uint64_t)(RLE_PATTERN_ALIGN - 1));
         u32 k = 0;
-        for (u32 o = written; o < upto; o += 16u * kWave, ++k) vstore(rso, o + 16u * lane < upto ? o + 16u * lane : kOOB, v, false);
+        // RLE_PATTERN_SHIFT: the stores start on the 128-byte line before `written` (lanes before it idle)
+        const u32 r = RLE_PATTERN_SHIFT ? ((rso.x >> 4) + (written >> 4)) & 7u : 0u;
+        const u32 nst = upto > written ? (upto - written + 16u * r + 16u * kWave - 1u) / (16u * kWave) : 0u;
+        for (; k < nst; ++k) {
+            const u32 a = written - 16u * r + 16u * (k * kWave + lane);   // (wraps below 0: never stored)
+            vstore(rso, a >= written && a < upto ? a : kOOB, v, false);
+        }
         written = upto;
         return k;
     });
