@@ -63,7 +63,10 @@ int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_off, const ui
                             uint32_t* d_status, uint32_t n, void* stream);
 
 /* Batched decode (RLEdecompress, src/rleCompression.c:47-62) of n buffers.
- * d_out_cap and d_status may be NULL. */
+ * d_out_cap and d_status may be NULL.  Batches of more than 4096 buffers are issued longest first:
+ * a small sort launch writes an issue-order array that the library keeps per (device, stream) and
+ * reuses (the first call on a stream allocates it, stream-ordered); calls from several host threads
+ * on one stream are serialised while they enqueue. */
 int rle_decode_batch_device(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                             void* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
                             const uint64_t* d_out_cap, uint32_t* d_status, uint32_t n, void* stream);
