@@ -308,8 +308,25 @@ __global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* 
 #define RLE_ORDER_LOCAL_PER 1
 #endif
 constexpr u32 kLocalPer = RLE_ORDER_LOCAL_PER, kLocalChunk = 256u * kLocalPer;
+#ifndef RLE_ORDER_DESC   // 1: the order holds each buffer's metadata in issue order (OrderDesc)
+#define RLE_ORDER_DESC 0
+#endif
+// RLE_ORDER_DESC: order[] entries are the buffers' metadata copied into issue order, so a decode
+// wave makes one dependent round trip for its buffer (its slot's descriptor) instead of two (its
+// slot's index, then the five metadata words at that index).
+struct OrderDesc {
+    uint64_t in_off, in_len, out_off, out_len, cap;
+    uint32_t b, pad;
+};
+static_assert(sizeof(OrderDesc) == 48u, "OrderDesc: three 16-byte stores");
+struct OrderMeta {   // the metadata arrays RLE_ORDER_DESC copies (cap: NULL = out_len)
+    const uint64_t* in_off;
+    const uint64_t* out_off;
+    const uint64_t* out_len;
+    const uint64_t* cap;
+};
 __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
-                                                              uint32_t* __restrict__ order) {
+                                                              uint32_t* __restrict__ order, OrderMeta meta) {
     __shared__ u32 lh[kOrderBuckets];
     __shared__ u32 wsum[4];
     constexpr u32 kPerT = kOrderBuckets / 256u;
@@ -338,7 +355,21 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
 #pragma unroll
     for (u32 j = 0; j < kLocalPer; ++j) {
         const u32 i = i0 + 256u * j;
-        if (i < n) order[blockIdx.x * kLocalChunk + lh[key[j]] + rank[j]] = i;
+        if (i >= n) continue;
+        const u32 place = blockIdx.x * kLocalChunk + lh[key[j]] + rank[j];
+        if (RLE_ORDER_DESC) {
+            OrderDesc d;
+            d.in_off = meta.in_off[i];
+            d.in_len = in_len[i];
+            d.out_off = meta.out_off[i];
+            d.out_len = meta.out_len[i];
+            d.cap = (meta.cap ? meta.cap : meta.out_len)[i];
+            d.b = i;
+            d.pad = 0u;
+            reinterpret_cast<OrderDesc*>(order)[place] = d;
+        } else {
+            order[place] = i;
+        }
     }
 }
 #ifndef RLE_ORDER_LOCAL
@@ -441,17 +472,36 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
             slot = (slot & 1u) ? n - 1u - (slot >> 1) : (slot >> 1);
         }
         if (!(RLE_ORDER_XCD && RLE_ORDER_MODE == 0) && RLE_ORDER_LOCAL && slot < n) slot = uniform(order_slot_local(slot, n));
-        b = slot < n ? uniform(order[slot]) : n;
+        if (RLE_ORDER_DESC && RLE_ORDER_LOCAL) {
+            b = slot;   // (the descriptor's index below)
+        } else {
+            b = slot < n ? uniform(order[slot]) : n;
+        }
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
     }
     // all five per-buffer words are loaded at once, unconditionally (index clamped; n >= 1)
-    const u32 bi = b < n ? b : 0u;
+    uint64_t C64, U64, cap, ioff, ooff;
+    if (RLE_ORDER_DESC && RLE_ORDER_LOCAL && order && RLE_ORDER_MODE != 3) {
+        const OrderDesc* od = reinterpret_cast<const OrderDesc*>(order) + (b < n ? b : 0u);
+        C64 = od->in_len;
+        U64 = od->out_len;
+        cap = od->cap;
+        ioff = od->in_off;
+        ooff = od->out_off;
+        b = b < n ? uniform(od->b) : n;
+    } else {
+        const u32 bi = b < n ? b : 0u;
+        const uint64_t* capp = out_cap ? out_cap : out_len;
+        C64 = in_len[bi];
+        U64 = out_len[bi];
+        cap = capp[bi];
+        ioff = in_off[bi];
+        ooff = out_off[bi];
+    }
     tl_mark(b, 0, lane);
     tl_put(b, 13, tl0, lane);
     tl_ids(b, lane);
-    const uint64_t* capp = out_cap ? out_cap : out_len;
-    const uint64_t C64 = in_len[bi], U64 = out_len[bi], cap = capp[bi], ioff = in_off[bi], ooff = out_off[bi];
     // all five loads in flight before the first use (else hipcc waits for in_off before issuing the
     // other four: two memory round trips ahead of the first tile's DMA instead of one)
     __builtin_amdgcn_sched_barrier(0);
@@ -620,18 +670,31 @@ __global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __res
         const u32 slot = blockIdx.x * kDecWaves + wid;
         const u32 place = RLE_ORDER_XCD ? order_place_xcd(blockIdx.x, gridDim.x, wid, n)
                                         : slot < n ? order_slot_local(slot, n) : n;
-        b = place < n ? uniform(order[uniform(place)]) : n;
+        b = place;
+        if (!RLE_ORDER_DESC) b = place < n ? uniform(order[uniform(place)]) : n;
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
     }
     b = uniform(b);
     if (b >= n) return;
     auto u64 = [](uint64_t x) { return (uint64_t)uniform((u32)x) | ((uint64_t)uniform((u32)(x >> 32)) << 32); };
-    const uint64_t C64 = u64(in_len[b]), U64 = u64(out_len[b]);
+    uint64_t C64, U64, ioff, ooff;
+    if (RLE_ORDER_DESC && order) {   // the decode's one round trip (its slot's descriptor)
+        const OrderDesc* od = reinterpret_cast<const OrderDesc*>(order) + b;
+        C64 = u64(od->in_len);
+        U64 = u64(od->out_len);
+        ioff = u64(od->in_off);
+        ooff = u64(od->out_off);
+    } else {
+        C64 = u64(in_len[b]);
+        U64 = u64(out_len[b]);
+        ioff = u64(in_off[b]);
+        ooff = u64(out_off[b]);
+    }
     if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) return;
     const u32 C = (u32)C64, U = (u32)U64;
-    const uint8_t* src = in + u64(in_off[b]);
-    uint8_t* dst = out + u64(out_off[b]);
+    const uint8_t* src = in + ioff;
+    uint8_t* dst = out + ooff;
     if (((uintptr_t)src | (uintptr_t)dst) & 15u) return;
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     const u32x4 rso = make_rsrc(dst, U);
@@ -879,11 +942,12 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     // more buffers than one residency round: issue them longest first (rle::dec_order_kernel)
     constexpr size_t kOrderExtra = RLE_ORDER_LOCAL ? 0u : 2u * rle::kOrderBuckets;
     OrderArray oa;   // [n] issue order, then [kOrderBuckets] counts and cursors
-    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, sizeof(uint32_t) * ((size_t)n + kOrderExtra));
+    const size_t entry = RLE_ORDER_DESC && RLE_ORDER_LOCAL ? sizeof(rle::OrderDesc) : sizeof(uint32_t);
+    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, entry * (size_t)n + sizeof(uint32_t) * kOrderExtra);
     uint32_t* order = oa.p;
     if (order && RLE_ORDER_LOCAL) {   // one launch, chunk-local sorts (rle::dec_order_local_kernel)
         hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
-                           s, d_in_len, n, order);
+                           s, d_in_len, n, order, rle::OrderMeta{d_in_off, d_out_off, d_out_len, d_out_cap});
     } else if (order) {
         uint32_t* hist = order + n;
         uint32_t* cursor = hist + rle::kOrderBuckets;
@@ -984,11 +1048,12 @@ extern "C" int rle_decode_pattern_device(const void* d_in, const uint64_t* d_in_
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len || n > kMaxGrid) return RLE_E_INVAL;
     const hipStream_t s = (hipStream_t)stream;
     OrderArray oa;   // the decode's issue order (decode_launch)
-    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, sizeof(uint32_t) * (size_t)n);
+    const size_t entry = RLE_ORDER_DESC ? sizeof(rle::OrderDesc) : sizeof(uint32_t);
+    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, entry * (size_t)n);
     uint32_t* order = oa.p;
     if (order)
         hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
-                           s, d_in_len, n, order);
+                           s, d_in_len, n, order, rle::OrderMeta{d_in_off, d_out_off, d_out_len, nullptr});
     hipLaunchKernelGGL(rle::pattern_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, n,
                        (const uint32_t*)order);
