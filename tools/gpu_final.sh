@@ -1,8 +1,8 @@
 #!/bin/bash
 # Final validation of a tree on one GPU box: the GPU tests, smoke(), two bench lines and a
-# rocprofv3 kernel-trace of a third.   usage: bash tools/gpu_final.sh
+# rocprofv3 kernel-trace of a third.   usage: bash tools/gpu_final.sh [TAG]
 set -o pipefail
-O=gpurun_out/r5fin3; mkdir -p $O
+O=gpurun_out/${1:-r5fin3}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
