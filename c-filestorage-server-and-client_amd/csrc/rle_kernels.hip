@@ -231,7 +231,10 @@ __device__ __forceinline__ u32 grouped_add(u32* hist, u32 key, bool on, u32 lane
 // workgroup.
 constexpr u32 kOrderPer = 4;
 constexpr u32 kOrderChunk = 256u * kOrderPer;
-template <u32 kPer = kOrderPer>   // buffers per thread (a workgroup's chunk: 256 kPer buffers)
+#ifndef RLE_ORDER_STABLE   // 1: ties inside a chunk keep index order (the waves rank one after another)
+#define RLE_ORDER_STABLE 0
+#endif
+template <u32 kPer = kOrderPer, bool kStable = false>   // buffers per thread (a workgroup's chunk: 256 kPer buffers)
 __device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kPer],
                                             u32 (&rank)[kPer]) {
     const u32 t = threadIdx.x, lane = t & (kWave - 1);
@@ -244,6 +247,14 @@ __device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, 
     __syncthreads();
 #pragma unroll
     for (u32 j = 0; j < kPer; ++j) key[j] = i0 + 256u * j < n ? order_key(len[j]) : 0u;
+    if (kStable && kPer == 1u) {   // wave w ranks after waves 0..w-1: equal keys in index order
+        const u32 wv = threadIdx.x / kWave;
+        for (u32 w = 0; w < 256u / kWave; ++w) {
+            if (wv == w) rank[0] = grouped_add(lh, key[0], i0 < n, lane);
+            __syncthreads();
+        }
+        return;
+    }
 #pragma unroll
     for (u32 j = 0; j < kPer; ++j) rank[j] = grouped_add(lh, key[j], i0 + 256u * j < n, lane);
     __syncthreads();
@@ -332,7 +343,7 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
     constexpr u32 kPerT = kOrderBuckets / 256u;
     const u32 t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
     u32 key[kLocalPer], rank[kLocalPer];
-    order_local<kLocalPer>(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
+    order_local<kLocalPer, RLE_ORDER_STABLE != 0>(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
     // thread t: the 8 buckets from B-1-8t down, in descending bucket order
     u32 c[kPerT], sum = 0u;
 #pragma unroll
@@ -376,10 +387,16 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
 #define RLE_ORDER_LOCAL 1
 #endif
 // The buffer a decode wave takes at issue slot s of an order made by dec_order_local_kernel.
+#ifndef RLE_ORDER_GROUP   // consecutive slots that take consecutive places of one chunk (1, 2, 4, ... 256)
+#define RLE_ORDER_GROUP 1
+#endif
 __device__ __forceinline__ u32 order_slot_local(u32 s, u32 n) {
     const u32 F = n / kLocalChunk;   // full chunks, interleaved; the partial one after them
     if (s >= F * kLocalChunk) return s;
-    return (s % F) * kLocalChunk + s / F;
+    constexpr u32 G = RLE_ORDER_GROUP;
+    static_assert(kLocalChunk % G == 0u, "RLE_ORDER_GROUP divides the chunk");
+    const u32 q = s / G;   // groups of G slots: group q takes places (q / F) G .. + G - 1 of chunk q % F
+    return (q % F) * kLocalChunk + (q / F) * G + s % G;
 }
 #ifndef RLE_ORDER_XCD   // 1: each XCD interleaves only the chunks of its own contiguous slice
 #define RLE_ORDER_XCD 0

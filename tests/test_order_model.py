@@ -103,3 +103,21 @@ def test_xcd_slices_are_longest_first_on_uniform_mixes():
         assert min(places) >= x * n // XCDS and max(places) < (x + 1) * n // XCDS
         keys = np.array([order_key(int(lengths[order[p]])) for p in places])
         assert np.all(np.diff(keys) <= 0), f"XCD {x} does not walk its slice longest first"
+
+
+def slot_to_place_grouped(s, n, G):
+    """order_slot_local with RLE_ORDER_GROUP = G."""
+    F = n // CHUNK
+    if s >= F * CHUNK:
+        return s
+    q = s // G
+    return (q % F) * CHUNK + (q // F) * G + s % G
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("n", [4097, 8195, 16384, 65537])
+def test_grouped_slots_cover_the_batch_once(n, G):
+    places = np.array([slot_to_place_grouped(s, n, G) for s in range(n)])
+    assert np.array_equal(np.sort(places), np.arange(n))
+    if G == 1:
+        assert all(slot_to_place(s, n) == places[s] for s in range(0, n, 97))
