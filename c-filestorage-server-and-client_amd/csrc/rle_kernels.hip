@@ -231,6 +231,9 @@ __device__ __forceinline__ u32 grouped_add(u32* hist, u32 key, bool on, u32 lane
 // workgroup.
 constexpr u32 kOrderPer = 4;
 constexpr u32 kOrderChunk = 256u * kOrderPer;
+#ifndef RLE_ORDER_SPREAD   // 1: ranks inside a bucket permuted per chunk (dec_order_local_kernel)
+#define RLE_ORDER_SPREAD 0
+#endif
 #ifndef RLE_ORDER_STABLE   // 1: ties inside a chunk keep index order (the waves rank one after another)
 #define RLE_ORDER_STABLE 0
 #endif
@@ -367,7 +370,16 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
     for (u32 j = 0; j < kLocalPer; ++j) {
         const u32 i = i0 + 256u * j;
         if (i >= n) continue;
-        const u32 place = blockIdx.x * kLocalChunk + lh[key[j]] + rank[j];
+        u32 r = rank[j];
+        if (RLE_ORDER_SPREAD) {
+            // a permutation inside the bucket (equal keys: longest first is kept) that differs from
+            // chunk to chunk: the chunks' same-rank slots, issued together, take different offsets
+            // inside their chunks, not buffers at a 16 MiB stride (r5at)
+            const u32 nvalid = n - blockIdx.x * kLocalChunk < kLocalChunk ? n - blockIdx.x * kLocalChunk : kLocalChunk;
+            const u32 m = (key[j] > 0u ? lh[key[j] - 1u] : nvalid) - lh[key[j]];
+            r = (r * 263u + blockIdx.x * 97u) % m;
+        }
+        const u32 place = blockIdx.x * kLocalChunk + lh[key[j]] + r;
         if (RLE_ORDER_DESC) {
             OrderDesc d;
             d.in_off = meta.in_off[i];
