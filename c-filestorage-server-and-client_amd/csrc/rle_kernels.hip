@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 
 namespace rle {
@@ -627,6 +628,10 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     }
 }
 
+}  // namespace rle
+#include "rle_round.h"   // the large-batch decode in rounds (dec_round_kernel)
+namespace rle {
+
 // ================================================================ synthetic generator
 __device__ __forceinline__ uint64_t xs64(uint64_t& s) {
     s ^= s << 13; s ^= s >> 7; s ^= s << 17;
@@ -852,6 +857,14 @@ constexpr uint32_t kDecChunksLarge = RLE_DEC_CHUNKS_LARGE;
 #ifndef RLE_WT_STATIC   // 1: the codec kernels instantiated per store policy (no run-time branch per store)
 #define RLE_WT_STATIC 1
 #endif
+// The large-batch decode in rounds (rle_round.h): waves per workgroup (4, 8 or 16; 0 off), for
+// batches past one residency round whose largest stream is at least kRoundMinIn bytes (the sized
+// entry points know it).  RLE_MI355X_DEC_ROUND overrides; tests switch it with rle_mi355x_set_dec_round.
+constexpr uint64_t kRoundMinIn = 8u * rle::kTileStep;
+std::atomic<int> g_dec_round{[] {
+    const char* e = getenv("RLE_MI355X_DEC_ROUND");
+    return e ? atoi(e) : 0;
+}()};
 bool dec_order_enabled() {
     static const bool on = !(getenv("RLE_MI355X_DEC_ORDER") && !strcmp(getenv("RLE_MI355X_DEC_ORDER"), "0"));
     return on;
@@ -963,7 +976,7 @@ extern "C" int rle_encode_batch_device(const void* d_in, const uint64_t* d_in_of
 namespace {
 int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, void* d_out,
                   const uint64_t* d_out_off, const uint64_t* d_out_len, const uint64_t* d_out_cap, uint32_t* d_status,
-                  uint32_t n, uint32_t flags, void* stream) {
+                  uint32_t n, uint32_t flags, void* stream, uint64_t max_in_len = 0) {
     if (n == 0) return RLE_OK;
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
@@ -985,9 +998,21 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
         hipLaunchKernelGGL(rle::dec_order_hist_kernel, g, dim3(256), 0, s, d_in_len, n, hist);
         hipLaunchKernelGGL(rle::dec_order_scatter_kernel, g, dim3(256), 0, s, d_in_len, n, hist, cursor, order);
     }
+    const uint32_t pol = store_policy(n, false);
+    const int rw = g_dec_round.load(std::memory_order_relaxed);
+    if (n > kDecRound && rw != 0 && max_in_len >= kRoundMinIn) {   // rounds of rw tiles per buffer
+        auto rk = rw == 4 ? (pol ? rle::dec_round_kernel<4, 96, true> : rle::dec_round_kernel<4, 96, false>)
+                : rw == 2 ? (pol ? rle::dec_round_kernel<2, 96, true> : rle::dec_round_kernel<2, 96, false>)
+                : rw == 16 ? (pol ? rle::dec_round_kernel<16, 64, true> : rle::dec_round_kernel<16, 64, false>)
+                           : (pol ? rle::dec_round_kernel<8, 96, true> : rle::dec_round_kernel<8, 96, false>);
+        const uint32_t threads = rle::kWave * (uint32_t)(rw == 2 || rw == 4 || rw == 16 ? rw : 8);
+        hipLaunchKernelGGL(rk, dim3(n), dim3(threads), 0, s, (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out,
+                           d_out_off, d_out_len, d_out_cap, d_status, n, pol | flags, (const uint32_t*)order);
+        if (!order_release(oa)) return RLE_E_HIP;
+        return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+    }
     // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD);
     // a few buffers (single drop-in calls): the deep tile ring
-    const uint32_t pol = store_policy(n, false);
     const bool large = n > kDecRound && kDecChunksLarge != rle::kDecChunks;
     auto kern = !RLE_WT_STATIC ? (large ? rle::decode_kernel<kDecChunksLarge> : rle::decode_kernel<rle::kDecChunks>)
                 : large ? (pol ? rle::decode_kernel<kDecChunksLarge, 0u, 1u> : rle::decode_kernel<kDecChunksLarge, 0u, 2u>)
@@ -1050,7 +1075,16 @@ extern "C" int rle_decode_batch_device_sized_flags(const void* d_in, const uint6
     const int c = rle_decode_coop_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n,
                                          max_in_len, max_out_len, flags, stream);
     if (c != 0) return c > 0 ? RLE_OK : c;
-    return decode_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n, flags, stream);
+    return decode_launch(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, d_out_cap, d_status, n, flags, stream,
+                         max_in_len);
+}
+
+// Tests / A-B: waves per workgroup of the large-batch decode in rounds (0 off, 4, 8, 16); -1 only
+// reads.  Returns the previous setting, or RLE_E_INVAL.
+extern "C" int rle_mi355x_set_dec_round(int waves) {
+    if (waves == -1) return g_dec_round.load(std::memory_order_relaxed);
+    if (waves != 0 && waves != 2 && waves != 4 && waves != 8 && waves != 16) return RLE_E_INVAL;
+    return g_dec_round.exchange(waves, std::memory_order_relaxed);
 }
 
 extern "C" int rle_decode_batch_device_sized(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,

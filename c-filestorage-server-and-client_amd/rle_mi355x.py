@@ -102,6 +102,8 @@ def lib():
     L.rle_append_prepare_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp]
     L.rle_mi355x_set_coop_mode.restype = ctypes.c_int
     L.rle_mi355x_set_coop_mode.argtypes = [ctypes.c_int]
+    L.rle_mi355x_set_dec_round.restype = ctypes.c_int
+    L.rle_mi355x_set_dec_round.argtypes = [ctypes.c_int]
     L.rle_copy_device.restype = ctypes.c_int
     L.rle_copy_device.argtypes = [vp, vp, ctypes.c_uint64, vp]
     L.rle_decode_pattern_device.restype = ctypes.c_int
@@ -336,6 +338,15 @@ def set_coop_mode(mode: int):
     when the launch is resident at once (-1, the default; RLE_MI355X_COOP sets it at load)."""
     if lib().rle_mi355x_set_coop_mode(int(mode)) != RLE_OK:
         raise RLEError(f"bad cooperative mode {mode}")
+
+
+def set_dec_round(waves: int) -> int:
+    """Waves per workgroup of the large-batch decode in rounds (csrc/rle_round.h): 0 off, 4, 8 or
+    16 (RLE_MI355X_DEC_ROUND sets it at load); -1 only reads.  Returns the previous setting."""
+    rc = lib().rle_mi355x_set_dec_round(int(waves))
+    if rc < 0:
+        raise RLEError(f"bad decode round width {waves}")
+    return rc
 
 
 def selftest() -> int:

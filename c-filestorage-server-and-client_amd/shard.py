@@ -21,16 +21,40 @@ def local_count(n_global: int, rank: int, world: int) -> int:
     return (n_global - rank + world - 1) // world if rank < n_global else 0
 
 
-def global_offsets(local_sizes: torch.Tensor, world: int) -> torch.Tensor:
-    """All-gather per-buffer compressed sizes (int64, one per local buffer, every rank holding the
-    same count) and return the exclusive scan of all sizes in global order: entry i is the byte
-    offset of global buffer i in the concatenated stream.  Collective: every rank must call it."""
+def padded_count(n_global: int, world: int) -> int:
+    """Entries every rank contributes to the size all-gather: ceil(n_global / world).  A global batch
+    that is not a multiple of the world size leaves the last ranks one buffer short; they pad with
+    zero-size entries, which sit at global positions >= n_global (k * world + r with k the last local
+    index), after every real buffer, so they add nothing to any real buffer's offset."""
+    return (n_global + world - 1) // world
+
+
+def pad_local(local_sizes: torch.Tensor, n_global: int, world: int) -> torch.Tensor:
+    """This rank's sizes padded with zeros to padded_count(n_global, world) entries."""
+    m = padded_count(n_global, world)
     n = local_sizes.numel()
+    if n == m:
+        return local_sizes.contiguous()
+    assert n == m - 1 or (n == 0 and m <= 1), f"rank holds {n} of {n_global} buffers over {world} ranks"
+    return torch.cat([local_sizes, torch.zeros(m - n, dtype=local_sizes.dtype, device=local_sizes.device)])
+
+
+def global_offsets(local_sizes: torch.Tensor, world: int, n_global: int = None) -> torch.Tensor:
+    """All-gather per-buffer compressed sizes (int64, one per local buffer) and return the exclusive
+    scan of all sizes in global order: entry i is the byte offset of global buffer i in the
+    concatenated stream (n_global entries).  n_global: the global batch size when it is not
+    world x the local count (ragged shards, padded by pad_local; default: every rank holds the same
+    count).  Collective: every rank must call it."""
+    n = local_sizes.numel()
+    if n_global is None:
+        n_global = n * world
     if world == 1:
         return torch.cumsum(local_sizes, 0) - local_sizes
-    gathered = torch.empty(world * n, dtype=local_sizes.dtype, device=local_sizes.device)
-    dist.all_gather_into_tensor(gathered, local_sizes.contiguous())
-    glob = gathered.view(world, n).t().reshape(-1)   # global order: i = k * world + r
+    padded = pad_local(local_sizes, n_global, world)
+    m = padded.numel()
+    gathered = torch.empty(world * m, dtype=local_sizes.dtype, device=local_sizes.device)
+    dist.all_gather_into_tensor(gathered, padded)
+    glob = gathered.view(world, m).t().reshape(-1)[:n_global]   # global order: i = k * world + r
     return torch.cumsum(glob, 0) - glob
 
 
@@ -97,7 +121,9 @@ class NativeExchange:
 
     def step(self, local_sizes: torch.Tensor, stream, slot: int = 0) -> torch.Tensor:
         """Issue one exchange on `stream` after the work issued on it so far, into result buffer
-        `slot` (0 or 1); returns the offsets tensor (complete in stream order)."""
+        `slot` (0 or 1); returns the offsets tensor (complete in stream order).  Ragged shards pass
+        their sizes padded with zeros to n = padded_count(n_global, world) (pad_local): the result's
+        first n_global entries are the offsets of the real buffers."""
         self.R.dist_gather_offsets(local_sizes, self.gathered[slot], self.offsets[slot], stream, ws=self.ws[slot])
         return self.offsets[slot]
 

@@ -213,6 +213,13 @@ int rle_dist_finalize(void);
  * otherwise. */
 int rle_mi355x_set_coop_mode(int mode);
 
+/* Tests / A-B: waves per workgroup of the large-batch decode in rounds (0 off, 4, 8 or 16): batches
+ * of more than 4096 buffers through the sized entry points whose max_in_len is at least 8 decode
+ * tiles (8064 bytes) decode one workgroup per buffer, its waves on consecutive tiles.
+ * RLE_MI355X_DEC_ROUND sets the initial value; -1 only reads it.  Returns the previous setting, or
+ * RLE_E_INVAL. */
+int rle_mi355x_set_dec_round(int waves);
+
 /* Measurement only (not the codec): copies nbytes (a multiple of 16, both pointers 16-byte aligned)
  * from d_src to d_dst on `stream` with a hand-written 16-byte-per-lane streaming kernel; bench.py
  * times it as the practical HBM ceiling of SURVEY.md §8(d).  RLE_E_INVAL on bad sizes. */

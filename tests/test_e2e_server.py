@@ -9,6 +9,15 @@ does: every returned file is byte-identical to its source, and the server's exit
 Battery 2 follows tests/test2.sh:6-30 (LRU eviction with MAXSTORAGECAP=1000000): big2 + randbig
 fit (942363 compressed bytes), writing big4 evicts randbig, which is decoded and shipped back
 (src/server.c:312-323) and must match its source.
+Battery LFU follows tests/test2.sh:36-64 (REPLACEMENTALGO=2): randbig read twice and big2 once, so
+writing big4 evicts big2, the least frequently used.  Battery victims follows tests/test2.sh:70-88:
+writing big1 (333334 compressed bytes) next to big2 + randbig evicts both.  Each checks the shipped
+files byte for byte and the server's exit statistics (max storage, files evicted).
+Battery concurrent follows the shape of tests/test3.sh (WORKERPOOLSIZE=8, several clients at once;
+the script's bigfiles/biggest* inputs are absent from the reference, .MISSING_LARGE_BLOBS): 8
+clients each write their own directory of 24 files (4-40 KiB random / zero / run-heavy, and the
+reference's smallfiles/small1, small7) and read every file back, all at once; every returned file
+must be byte-identical to its source.
 """
 import json
 import os
@@ -38,9 +47,9 @@ def _stage_files(tmp):
         dst = os.path.join(d, rel)
         os.makedirs(os.path.dirname(dst), exist_ok=True)
         shutil.copyfile(os.path.join(GOLDEN, "dummyFiles", rel.replace("/", "__")), dst)
-    for rel in ("bigfiles/big2", "bigfiles/big4"):
+    for rel, U in (("bigfiles/big2", 360000), ("bigfiles/big4", 360000), ("bigfiles/big1", 1000000)):
         with open(os.path.join(d, rel), "wb") as f:
-            f.write(bytes(360000))
+            f.write(bytes(U))
     return d
 
 
@@ -80,6 +89,12 @@ class Server:
 
 def _max_storage(text):
     m = re.search(r"Max total storage size reached: (\d+) bytes", text)
+    assert m, text[-2000:]
+    return int(m.group(1))
+
+
+def _victims(text):
+    m = re.search(r"Number of files that have been evicted from the cache: (\d+)", text)
     assert m, text[-2000:]
     return int(m.group(1))
 
@@ -124,9 +139,127 @@ def battery2(exe, tmp, env=None, settle=0.0):
             wall)
 
 
+def battery_lfu(exe, tmp, env=None):
+    """tests/test2.sh:36-64: LFU (REPLACEMENTALGO=2); big2 is read once, randbig twice, so big4
+    evicts big2."""
+    files = _stage_files(tmp)
+    srv = Server(exe, tmp, {"MAXSTORAGECAP": 1000000, "MAXFILECOUNT": 10, "WORKERPOOLSIZE": 4,
+                            "REPLACEMENTALGO": 2}, env)
+    b = lambda n: os.path.join(files, "bigfiles", n)
+    try:
+        srv.client("-W", f"{b('big2')},{b('randbig')}")
+        srv.client("-r", b("randbig"), "-d", os.path.join(tmp, "readback", "1"))
+        srv.client("-r", b("randbig"), "-d", os.path.join(tmp, "readback", "2"))
+        srv.client("-r", b("big2"), "-d", os.path.join(tmp, "readback", "3"))
+        srv.client("-W", b("big4"), "-D", os.path.join(tmp, "evicted2"))
+    finally:
+        text = srv.stop()
+    return _max_storage(text), _victims(text), _returned(os.path.join(tmp, "evicted2")), \
+        _returned(os.path.join(tmp, "readback"))
+
+
+def battery_victims(exe, tmp, env=None):
+    """tests/test2.sh:70-88: big1 (C = 333334) does not fit next to big2 + randbig (942363 of
+    1000000): both are evicted, decoded and shipped back in one write."""
+    files = _stage_files(tmp)
+    srv = Server(exe, tmp, {"MAXSTORAGECAP": 1000000, "MAXFILECOUNT": 10, "WORKERPOOLSIZE": 4,
+                            "REPLACEMENTALGO": 2}, env)
+    b = lambda n: os.path.join(files, "bigfiles", n)
+    try:
+        srv.client("-W", f"{b('big2')},{b('randbig')}")
+        srv.client("-W", b("big1"), "-D", os.path.join(tmp, "evicted3"))
+        srv.client("-r", b("big1"), "-d", os.path.join(tmp, "readback"))
+    finally:
+        text = srv.stop()
+    return _max_storage(text), _victims(text), _returned(os.path.join(tmp, "evicted3")), \
+        _returned(os.path.join(tmp, "readback"))
+
+
+def _concurrent_files(tmp, c, nfiles, rnd):
+    d = os.path.join(tmp, f"c{c}")
+    os.makedirs(d, exist_ok=True)
+    files = {}
+    for k in range(nfiles):
+        if k < 2:   # the reference's small files, once per client directory
+            name = ("smallfiles__small1", "smallfiles__small7")[k]
+            b = open(os.path.join(GOLDEN, "dummyFiles", name), "rb").read()
+        else:
+            U = rnd.choice([4096, 8192, 16384, 40000])
+            kind = k % 3
+            b = bytes(U) if kind == 1 else (rnd.randbytes(U) if kind == 0 else
+                                            b"".join(bytes([rnd.randrange(256)]) * rnd.randrange(1, 12)
+                                                     for _ in range(U // 4))[:U])
+        p = os.path.join(d, f"f{c}_{k}")
+        with open(p, "wb") as f:
+            f.write(b)
+        files[p] = b
+    return d, files
+
+
+def battery_concurrent(exe, tmp, env=None, clients=8, nfiles=24):
+    """tests/test3.sh's shape: 8 workers, `clients` clients at once, each writing its directory (-w)
+    and reading its files back (-r); returns {path: (source, [returned copies])}."""
+    import random
+    import threading
+    rnd = random.Random(3)
+    dirs = [_concurrent_files(os.path.join(tmp, "src"), c, nfiles, rnd) for c in range(clients)]
+    srv = Server(exe, tmp, {"MAXSTORAGECAP": 512000000, "MAXFILECOUNT": 10000, "WORKERPOOLSIZE": 8}, env)
+    errs = []
+
+    def client(c, d, names):
+        try:
+            srv.client("-w", f"{d},0")
+            srv.client("-r", ",".join(names), "-d", os.path.join(tmp, f"out{c}"))
+        except Exception as e:   # noqa: BLE001 (reported below)
+            errs.append(repr(e))
+
+    try:
+        th = [threading.Thread(target=client, args=(c, d, sorted(fs))) for c, (d, fs) in enumerate(dirs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        text = srv.stop()
+    assert not errs, errs[:3]
+    got = {}
+    for c in range(clients):
+        got.update({k: v for k, v in _returned(os.path.join(tmp, f"out{c}")).items()})
+    return {p: (b, got.get(os.path.basename(p), [])) for _, fs in dirs for p, b in fs.items()}, _max_storage(text)
+
+
+def _check_lfu(res):
+    stat, victims, ev, rb = res
+    assert stat == 942363 and victims == 1
+    assert list(ev) == ["big2"] and ev["big2"] == [bytes(360000)]
+    assert rb["randbig"] == [_src("randbig")] * 2 and rb["big2"] == [bytes(360000)]
+
+
+def _check_victims(res):
+    stat, victims, ev, rb = res
+    assert stat == 942363 and victims == 2
+    assert sorted(ev) == ["big2", "randbig"]
+    assert ev["big2"] == [bytes(360000)] and ev["randbig"] == [_src("randbig")]
+    assert rb["big1"] == [bytes(1000000)]
+
+
+def _check_concurrent(res):
+    files, stat = res
+    bad = [p for p, (b, copies) in files.items() if copies != [b]]
+    assert not bad, (len(bad), bad[:3])
+    assert stat == sum(len(O_encode(b)) for b, _ in files.values())
+
+
+def O_encode(b):
+    import rle_oracle as O
+    return O.encode(b)
+
+
 def _src(name):
     if name in ("big2", "big4"):
         return bytes(360000)
+    if name == "big1":
+        return bytes(1000000)
     rel = {"file1": "file1", "file2": "file2", "rec1": "rec/rec1", "rec2": "rec/rec2", "randbig": "bigfiles/randbig"}
     return open(os.path.join(GOLDEN, "dummyFiles", rel[name].replace("/", "__")), "rb").read()
 
@@ -152,6 +285,9 @@ def test_e2e_reference_server(tmp_path):
     _need(exe)
     _check_battery1(battery1(exe, str(tmp_path / "b1")))
     _check_battery2(battery2(exe, str(tmp_path / "b2")))
+    _check_lfu(battery_lfu(exe, str(tmp_path / "lfu")))
+    _check_victims(battery_victims(exe, str(tmp_path / "victims")))
+    _check_concurrent(battery_concurrent(exe, str(tmp_path / "conc")))
 
 
 @pytest.mark.gpu
@@ -165,3 +301,23 @@ def test_e2e_gpu_server(tmp_path):
     assert st["calls_compress"] >= 4 and st["calls_decompress"] >= 6   # 4 writes; 6 reads
     _check_battery2(battery2(exe, str(tmp_path / "b2")))
     print("e2e gpu battery1 wall %.3fs dropin %s" % (res1[3], st))
+
+
+@pytest.mark.gpu
+def test_e2e_gpu_server_lfu_and_victims(tmp_path):
+    """tests/test2.sh's LFU battery (:36-64) and multiple-victims battery (:70-88) against the
+    drop-in: evicted files decoded on the GPU (src/server.c:317) and shipped back byte-identical."""
+    exe = os.path.join(BIN, "server_gpu")
+    _need(exe)
+    _check_lfu(battery_lfu(exe, str(tmp_path / "lfu")))
+    _check_victims(battery_victims(exe, str(tmp_path / "victims")))
+
+
+@pytest.mark.gpu
+def test_e2e_gpu_server_concurrent_workers(tmp_path):
+    """tests/test3.sh's shape against the drop-in: 8 workers serving 8 clients at once, concurrent
+    compress and decompress calls from the worker threads, every returned file byte-identical and
+    the max-storage statistic equal to the oracle's compressed sizes."""
+    exe = os.path.join(BIN, "server_gpu")
+    _need(exe)
+    _check_concurrent(battery_concurrent(exe, str(tmp_path / "conc")))

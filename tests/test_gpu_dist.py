@@ -47,6 +47,43 @@ def test_exchange_step_one_rank():
         R.dist_finalize()
 
 
+@pytest.mark.parametrize("world,n_global", [(3, 1000), (8, 131071), (2, 4097)])
+def test_offsets_kernel_ragged_padded(world, n_global):
+    """Ragged shards (shard.pad_local): each rank's sizes padded with zeros to ceil(n_global / world);
+    the reorder + scan kernel over the padded all-gather gives, in its first n_global entries, the
+    single-process exclusive scan of the real sizes."""
+    import shard
+    rng = np.random.default_rng(n_global)
+    sizes = rng.integers(0, 70000, size=n_global, dtype=np.int64)
+    m = shard.padded_count(n_global, world)
+    rows = [shard.pad_local(torch.from_numpy(sizes[r::world].copy()), n_global, world).numpy() for r in range(world)]
+    g = np.concatenate(rows)
+    d_g = torch.from_numpy(g).to(DEV)
+    d_o = torch.full((world * m,), -1, dtype=torch.int64, device=DEV)
+    R.dist_offsets(d_g, world, m, d_o)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_o.cpu().numpy()[:n_global], np.cumsum(sizes) - sizes)
+
+
+def test_exchange_step_one_rank_padded_count():
+    """The one-rank RCCL rehearsal with a padded count: zero-size entries past the real buffers
+    leave every real offset equal to the cumsum of the real sizes."""
+    uid = R.dist_unique_id()
+    R.dist_init(uid, 0, 1)
+    try:
+        n_real, n = 4093, 4096
+        sizes = torch.randint(1, 6000, (n,), dtype=torch.int64, device=DEV)
+        sizes[n_real:] = 0
+        gathered = torch.empty_like(sizes)
+        offsets = torch.full((n,), -1, dtype=torch.int64, device=DEV)
+        R.dist_gather_offsets(sizes, gathered, offsets, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        real = sizes[:n_real]
+        assert torch.equal(offsets[:n_real], torch.cumsum(real, 0) - real)
+    finally:
+        R.dist_finalize()
+
+
 def test_exchange_captured_in_graph_one_rank():
     """The graph form bench.py uses at N > 1: the exchange issued on a branch stream inside a HIP
     graph capture (fork / join by events), replayed several times, gives the same offsets."""

@@ -36,7 +36,9 @@ def _worker(rank, world, port, n_global, q):
             y = O.encode(x)
             streams[i] = y
             sizes.append(len(y))
-        glob = shard.global_offsets(torch.tensor(sizes, dtype=torch.int64), world)
+        ragged = n_global % world != 0
+        glob = shard.global_offsets(torch.tensor(sizes, dtype=torch.int64), world,
+                                    n_global=n_global if ragged else None)
         mine = shard.my_offsets(glob, rank, world)
         q.put((rank, {i: (int(o), s) for i, o, s in zip(idx, mine.tolist(), [streams[i] for i in idx])},
                glob.tolist()))
@@ -44,16 +46,17 @@ def _worker(rank, world, port, n_global, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_round_robin_shards_and_global_offsets(world):
-    n_global = 64   # divisible by world: every rank holds the same count (the collective's contract)
+@pytest.mark.parametrize("world,n_global", [(2, 64), (3, 1000), (2, 63), (3, 2)])
+def test_round_robin_shards_and_global_offsets(world, n_global):
+    """Equal shards (64 over 2) and ragged ones (1000 over 3, 63 over 2, 2 over 3: a rank with no
+    buffer), each rank's sizes padded with zeros to ceil(n_global / world) for the all-gather."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_global, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -81,3 +84,23 @@ def test_shard_indices_cover_once():
         allidx = sorted(i for r in range(world) for i in shard.shard_indices(n, r, world))
         assert allidx == list(range(n))
         assert sum(shard.local_count(n, r, world) for r in range(world)) == n
+
+
+def test_padding_rule_matches_single_process_cumsum():
+    """The padded all-gather's layout (no processes): every rank's sizes padded to ceil(n / world),
+    interleaved in global order and cut at n, equals the single-process exclusive scan."""
+    rng = np.random.default_rng(3)
+    for world in (1, 2, 3, 7, 8):
+        for n in (1, 2, 7, 8, 9, 1000, 1001, 1023):
+            sizes = rng.integers(0, 100000, size=n)
+            m = shard.padded_count(n, world)
+            rows = []
+            for r in range(world):
+                loc = torch.tensor(sizes[r::world], dtype=torch.int64)
+                assert loc.numel() == shard.local_count(n, r, world)
+                rows.append(shard.pad_local(loc, n, world))
+            gathered = torch.stack(rows)              # [world, m], as all_gather_into_tensor lays it out
+            glob = gathered.t().reshape(-1)[:n]
+            assert glob.numel() == n and m * world - n < world
+            off = (torch.cumsum(glob, 0) - glob).numpy()
+            assert np.array_equal(off, np.cumsum(sizes) - sizes), (world, n)
