@@ -721,7 +721,8 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
         if (tiles <= 4) RLE_DEC_COOP(4, 32768);
         else if (tiles <= 8) RLE_DEC_COOP(8, 32768);
         else if (tiles <= 16) RLE_DEC_COOP(16, 32768);
-        else RLE_DEC_COOP_R(16, 32768, 3);
+        else if (tiles <= 48) RLE_DEC_COOP_R(16, 32768, 3);
+        else RLE_DEC_COOP_R(16, 32768, 4);   // (a worst-case 32 KiB stream: up to 49 tiles)
     } else if (tiles > 16) {   // (random 16 KiB: 17 tiles)
         RLE_DEC_COOP_R(16, 16384, 2);
     } else if (max_out_len <= 4096u) {

@@ -283,7 +283,10 @@ void free_ctx(void* p) {
     (void)hipFree(c->d_bm);
     for (hipEvent_t e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->s) (void)hipStreamDestroy(c->s);
+    if (c->s) {
+        (void)rle_decode_release_stream(c->s);   // (the issue-order array of large RLEdecompressN batches)
+        (void)hipStreamDestroy(c->s);
+    }
     delete c;
     pthread_mutex_unlock(&g_exit_lock);
 }
@@ -523,7 +526,8 @@ __attribute__((constructor)) void preinit_start() {
     if (const char* t = getenv("RLE_MI355X_TRACE"))
         if (*t) g_trace = static_cast<TraceRec*>(calloc(kTraceMax, sizeof(TraceRec)));
     const char* e = getenv("RLE_MI355X_PREINIT");
-    if (e ? atoi(e) <= 0 : !needed_by_main()) return;
+    const bool linked = needed_by_main();
+    if (e ? atoi(e) <= 0 : !linked) return;
     pthread_atfork(preinit_atfork_prepare, preinit_atfork_parent, preinit_atfork_child);
     atexit(preinit_exit);
     pthread_mutex_lock(&g_pool_m);
@@ -536,8 +540,13 @@ __attribute__((constructor)) void preinit_start() {
     // cold battery 3).  The process starts that much later instead (tools/e2e_compare.py
     // reports both servers' start-up).  Bounded: after RLE_MI355X_PREINIT_WAIT_MS (default 5000; 0 =
     // do not wait, round 4's behaviour) main() starts anyway and the thread goes on in the background.
-    long wait_ms = 5000;
-    if (const char* w = getenv("RLE_MI355X_PREINIT_WAIT_MS")) wait_ms = atol(w);
+    // Only where the library is among the main program's DT_NEEDED entries: a dlopen()ed
+    // library's constructor runs under the loader lock, and a dlopen inside the HIP runtime's start-up
+    // on the thread would wait for that lock while this constructor waits for the thread, until the
+    // timeout; so a dlopen()ed library (RLE_MI355X_PREINIT > 0) starts the thread and returns.
+    long wait_ms = linked ? 5000 : 0;
+    if (const char* w = getenv("RLE_MI355X_PREINIT_WAIT_MS"))
+        if (linked) wait_ms = atol(w);
     if (wait_ms > 0 && g_pre_started.load()) {
         timespec until;
         clock_gettime(CLOCK_REALTIME, &until);

@@ -875,28 +875,51 @@ bool dec_order_enabled() {
 #endif
 // The issue order's device array.  A hipFreeAsync + hipMallocAsync pair per launch left a 5.8 us gap
 // on the queue between back-to-back large decodes (profiles/r5an_order_gap.md); instead each
-// (device, stream) keeps a grow-only array (kOrderStreams of them; more streams, and launches being
-// captured into a graph, take the per-launch pair).  The lock is held until the order and decode
+// (device, stream handle) keeps a grow-only array in one of kOrderStreams slots (launches being
+// captured into a graph take the per-launch pair).  The lock is held until the order and decode
 // kernels are both enqueued, so host threads sharing a stream cannot interleave their launches.
+// A handle does not always name one queue: hipStreamPerThread is a different stream in
+// every thread, and a destroyed stream's handle can come back for a new stream while the old one's
+// decode still reads the array.  So every slot records an event after its last decode, and the
+// next launch on the slot makes its stream wait for it before the order kernel rewrites the array:
+// on one queue that wait is already satisfied by stream order; across queues it keeps the array's
+// users in turn.  When all slots are taken, the least recently used one is handed over (its array
+// freed behind its event on the new stream); rle_decode_release_stream frees a stream's slot.
+struct OrderSlot {
+    int dev = -1;
+    hipStream_t s = nullptr;
+    uint32_t* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;   // recorded after the slot's last decode launch
+    bool recorded = false;
+    uint64_t last = 0;           // LRU clock
+};
 struct OrderArray {
     uint32_t* p = nullptr;
     hipStream_t s = nullptr;
-    bool pooled = false;   // a per-launch array: freed on the stream after the decode
+    bool pooled = false;        // a per-launch array: freed on the stream after the decode
+    OrderSlot* slot = nullptr;  // a cached array: its event is recorded after the decode
     std::unique_lock<std::mutex> lk;
     ~OrderArray() {   // early returns (order_release clears p)
         if (pooled && p) (void)hipFreeAsync(p, s);
     }
 };
 constexpr uint32_t kOrderStreams = 16;
-struct OrderSlot {
-    int dev;
-    hipStream_t s;
-    uint32_t* p;
-    size_t cap;
-};
 std::mutex g_order_mu;
 OrderSlot g_order_slots[kOrderStreams];
-uint32_t g_order_count = 0;
+uint64_t g_order_clock = 0;
+// (g_order_mu held) the slot's array released behind its last decode, on stream `s`
+void order_slot_drop(OrderSlot& e, hipStream_t s) {
+    if (e.p) {
+        if (e.recorded) (void)hipStreamWaitEvent(s, e.done, 0);
+        (void)hipFreeAsync(e.p, s);
+    }
+    e.p = nullptr;
+    e.cap = 0;
+    e.recorded = false;
+    e.s = nullptr;
+    e.dev = -1;
+}
 void order_acquire(OrderArray& o, hipStream_t s, size_t bytes) {
     o.s = s;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
@@ -905,13 +928,32 @@ void order_acquire(OrderArray& o, hipStream_t s, size_t bytes) {
         hipGetDevice(&dev) == hipSuccess) {
         o.lk = std::unique_lock<std::mutex>(g_order_mu);
         OrderSlot* e = nullptr;
-        for (uint32_t i = 0; i < g_order_count && !e; ++i)
-            if (g_order_slots[i].s == s && g_order_slots[i].dev == dev) e = &g_order_slots[i];
-        if (!e && g_order_count < kOrderStreams) {
-            e = &g_order_slots[g_order_count++];
-            *e = OrderSlot{dev, s, nullptr, 0};
+        for (uint32_t i = 0; i < kOrderStreams && !e; ++i)
+            if (g_order_slots[i].p && g_order_slots[i].s == s && g_order_slots[i].dev == dev) e = &g_order_slots[i];
+        if (!e) {   // a free slot of this device's, else the least recently used one
+            for (uint32_t i = 0; i < kOrderStreams; ++i) {
+                OrderSlot& c = g_order_slots[i];
+                if (!e || (!c.p && e->p) || (!!c.p == !!e->p && c.last < e->last)) e = &c;
+            }
+            if (e->p && e->dev != dev) e = nullptr;   // (another device's array: not freed from here)
+            if (e) {
+                order_slot_drop(*e, s);
+                e->dev = dev;
+                e->s = s;
+            }
         }
-        if (e && e->cap < bytes) {   // grow: the old array is freed behind this stream's earlier decodes
+        if (e && !e->done && hipEventCreateWithFlags(&e->done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            e->done = nullptr;
+            e = nullptr;
+        }
+        if (e) {
+            if (e->recorded && hipStreamWaitEvent(s, e->done, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                e = nullptr;
+            }
+        }
+        if (e && e->cap < bytes) {   // grow: the old array is freed behind the earlier decodes (the wait above)
             const size_t cap = bytes > (1u << 20) ? bytes : (1u << 20);
             uint32_t* q = nullptr;
             if (hipMallocAsync((void**)&q, cap, s) == hipSuccess) {
@@ -925,6 +967,7 @@ void order_acquire(OrderArray& o, hipStream_t s, size_t bytes) {
         }
         if (e) {
             o.p = e->p;
+            o.slot = e;
             return;
         }
         o.lk.unlock();
@@ -937,9 +980,21 @@ void order_acquire(OrderArray& o, hipStream_t s, size_t bytes) {
     }
     o.pooled = true;
 }
-// After the decode's launch: frees a per-launch array on the stream (RLE_E_HIP when that fails).
+// After the decode's launch: frees a per-launch array on the stream, or records the cached slot's
+// event (RLE_E_HIP when that fails).
 bool order_release(OrderArray& o) {
-    const bool ok = !(o.pooled && o.p && hipFreeAsync(o.p, o.s) != hipSuccess);
+    bool ok = !(o.pooled && o.p && hipFreeAsync(o.p, o.s) != hipSuccess);
+    if (o.slot) {
+        if (hipEventRecord(o.slot->done, o.s) == hipSuccess) {
+            o.slot->recorded = true;
+        } else {
+            (void)hipGetLastError();
+            order_slot_drop(*o.slot, o.s);   // (no event: the array goes behind this launch)
+            ok = false;
+        }
+        o.slot->last = ++g_order_clock;
+        o.slot = nullptr;
+    }
     o.p = nullptr;
     if (o.lk.owns_lock()) o.lk.unlock();
     return ok;
@@ -1081,6 +1136,19 @@ extern "C" int rle_decode_batch_device_sized_flags(const void* d_in, const uint6
 
 // Tests / A-B: waves per workgroup of the large-batch decode in rounds (0 off, 4, 8, 16); -1 only
 // reads.  Returns the previous setting, or RLE_E_INVAL.
+// Frees the issue-order array cached for `stream` on the current device (behind the stream's earlier
+// decodes); a caller about to destroy a stream, or done with a thread's per-thread stream, calls it.
+extern "C" int rle_decode_release_stream(void* stream) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return RLE_E_HIP;
+    std::lock_guard<std::mutex> lk(g_order_mu);
+    for (uint32_t i = 0; i < kOrderStreams; ++i) {
+        OrderSlot& e = g_order_slots[i];
+        if (e.p && e.s == (hipStream_t)stream && e.dev == dev) order_slot_drop(e, (hipStream_t)stream);
+    }
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
+
 extern "C" int rle_mi355x_set_dec_round(int waves) {
     if (waves == -1) return g_dec_round.load(std::memory_order_relaxed);
     if (waves != 0 && waves != 2 && waves != 4 && waves != 8 && waves != 16) return RLE_E_INVAL;

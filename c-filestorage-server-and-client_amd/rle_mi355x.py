@@ -102,6 +102,8 @@ def lib():
     L.rle_append_prepare_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp]
     L.rle_mi355x_set_coop_mode.restype = ctypes.c_int
     L.rle_mi355x_set_coop_mode.argtypes = [ctypes.c_int]
+    L.rle_decode_release_stream.restype = ctypes.c_int
+    L.rle_decode_release_stream.argtypes = [vp]
     L.rle_mi355x_set_dec_round.restype = ctypes.c_int
     L.rle_mi355x_set_dec_round.argtypes = [ctypes.c_int]
     L.rle_copy_device.restype = ctypes.c_int
@@ -203,11 +205,21 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+STREAM_PER_THREAD = 2   # hipStreamPerThread ((hipStream_t)2, hip_runtime_api.h)
+
+
 def _stream_ptr(stream):
     if stream is None:
         import torch
         stream = torch.cuda.current_stream()
+    if isinstance(stream, int):   # a raw handle (tests: hipStreamPerThread)
+        return ctypes.c_void_p(stream)
     return ctypes.c_void_p(stream.cuda_stream)
+
+
+def release_stream(stream):
+    """Free the issue-order array the library keeps for `stream` (rle_decode_release_stream)."""
+    _check(lib().rle_decode_release_stream(_stream_ptr(stream)), "rle_decode_release_stream")
 
 
 def encode_batch(d_in, in_off, in_len, d_out, out_off, out_len, status=None, stream=None, max_len=None, flags=0):
@@ -415,17 +427,24 @@ def _ws(ws):
 # Workspaces made for calls that pass none: the scan kernels run on `stream` (or the
 # comm stream, or a captured graph replays them) after the call returns, so a temporary torch tensor
 # could be handed to another tensor by the caching allocator while they still use it.  One workspace
-# per (device, n, stream, slot) instead, kept for the life of the process: calls on one stream run
-# in order, and calls that may run at once (different streams or slots) get different workspaces.
+# per (device, stream, slot) instead, kept for the life of the process: calls on one stream run in
+# order, and calls that may run at once (different streams or slots) get different workspaces.  It
+# grows when a larger n needs more (keyed on n as well, callers whose n changed from step
+# to step grew device memory without bound); the replaced tensor is marked as used by the stream
+# (record_stream), so the allocator hands it out again only after the work issued on it so far.
 _WS_CACHE = {}
 
 
 def _default_ws(n, device, stream, slot):
     import torch
     dev = torch.device(device)
-    key = (dev.type, dev.index, int(n), _stream_ptr(stream).value or 0, slot)
+    key = (dev.type, dev.index, _stream_ptr(stream).value or 0, slot)
+    need = max(1, int(lib().rle_dist_workspace_bytes(int(n))) // 8)
     ws = _WS_CACHE.get(key)
-    if ws is None:
+    if ws is None or ws.numel() < need:
+        if ws is not None:
+            s = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.current_stream(dev)
+            ws.record_stream(s)
         ws = _WS_CACHE[key] = dist_workspace(n, dev)
     return ws
 

@@ -220,6 +220,12 @@ int rle_mi355x_set_coop_mode(int mode);
  * RLE_E_INVAL. */
 int rle_mi355x_set_dec_round(int waves);
 
+/* Large decodes (more than 4096 buffers) keep their issue-order array per (device, stream handle),
+ * up to 16 of them, the least recently used handed over when a new stream needs one; every array
+ * is used in turn across the queues a handle may name (hipStreamPerThread, a reused handle).  This
+ * frees the array kept for `stream` on the current device, behind the work already issued on it. */
+int rle_decode_release_stream(void* stream);
+
 /* Measurement only (not the codec): copies nbytes (a multiple of 16, both pointers 16-byte aligned)
  * from d_src to d_dst on `stream` with a hand-written 16-byte-per-lane streaming kernel; bench.py
  * times it as the practical HBM ceiling of SURVEY.md §8(d).  RLE_E_INVAL on bad sizes. */

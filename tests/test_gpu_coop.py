@@ -199,3 +199,13 @@ def test_completion_flag_launches_same_bytes(coop):
             assert got[i] == xs[i], i
         assert st[len(xs)] & R.RLE_STATUS_SERIAL and st[len(xs) + 1] == R.RLE_STATUS_SHORT
     R.set_coop_mode(1)
+
+
+def test_worst_case_32k_streams_take_four_rounds():
+    """a 16-32 KiB buffer whose stream is past 48 tiles (all runs of length 2: C = 1.5 U,
+    up to 49152 bytes = 49 tiles) now takes the four-round workgroup (dec_coop_kernel<16, 32768, 4>)
+    instead of the one-wave fallback; sizes around the 48-tile edge, bit-exact."""
+    xs = []
+    for U in (32768, 32767, 32256, 32254, 32250, 30000, 24000, 16385):
+        xs.append(O.gen(4, U, U))   # kind 4: pairs (the 1.5x worst case)
+    coop_parity(xs)

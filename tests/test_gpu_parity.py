@@ -462,6 +462,69 @@ def test_large_decodes_from_threads_and_streams():
         assert int(stats[k].abs().sum().item()) == 0
 
 
+def test_large_decodes_per_thread_stream_and_slot_turnover():
+    """the issue-order arrays are cached per stream HANDLE.  Two host threads decode large
+    batches on hipStreamPerThread (one handle, a different queue in each thread), while a third
+    cycles through 20 fresh torch streams (more than the 16 slots: least-recently-used slots are
+    handed over, rle_decode_release_stream frees some); every output bit-exact."""
+    rng = np.random.default_rng(44)
+    n = 6000
+    xs = [O.gen(i % 5, 5 * i + 1, int(rng.integers(0, 1800))) for i in range(n)]
+    ys = [O.encode(x) for x in xs]
+    in_offs, in_total = R.layout([len(y) for y in ys])
+    host = np.zeros(in_total, np.uint8)
+    for y, o in zip(ys, in_offs):
+        host[o:o + len(y)] = np.frombuffer(y, np.uint8)
+    d_c = torch.from_numpy(host).to(DEV)
+    sizes = [len(x) for x in xs]
+    out_offs, out_total = R.layout(sizes)
+    want = np.full(out_total, POISON, np.uint8)
+    for x, o in zip(xs, out_offs):
+        want[o:o + len(x)] = np.frombuffer(x, np.uint8)
+    coffs, clens, uoffs, ulens = _i64(in_offs), _i64([len(y) for y in ys]), _i64(out_offs), _i64(sizes)
+    nthreads, reps = 3, 6
+    outs = [[torch.full((out_total + 16,), POISON, dtype=torch.uint8, device=DEV) for _ in range(reps)]
+            for _ in range(nthreads)]
+    stats = [[torch.full((n,), 0x7777, dtype=torch.int32, device=DEV) for _ in range(reps)] for _ in range(nthreads)]
+    fresh = [torch.cuda.Stream(DEV) for _ in range(20)]
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(k):
+        try:
+            torch.cuda.set_device(0)
+            for r in range(reps):
+                m = (4200, n, 5000, n, 4500, n)[r]
+                if k < 2:
+                    R.decode_batch(d_c, coffs[:m], clens[:m], outs[k][r], uoffs[:m], ulens[:m], None, stats[k][r][:m],
+                                   stream=R.STREAM_PER_THREAD)
+                else:
+                    for j, st in enumerate(fresh):
+                        R.decode_batch(d_c, coffs[:m], clens[:m], outs[k][r], uoffs[:m], ulens[:m], None,
+                                       stats[k][r][:m], stream=st)
+                        if j % 3 == 0:
+                            R.release_stream(st)
+            if k < 2:
+                R.release_stream(R.STREAM_PER_THREAD)
+        except Exception as e:   # noqa: BLE001 (reported below)
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(nthreads):
+        for r in range(reps):
+            m = (4200, n, 5000, n, 4500, n)[r]
+            got = outs[k][r].cpu().numpy()[:out_total]
+            end = out_offs[m] if m < n else out_total
+            assert np.array_equal(got[:end], want[:end]), f"thread {k} rep {r}: decoded bytes differ"
+            assert int(stats[k][r][:m].abs().sum().item()) == 0
+
+
 @pytest.mark.parametrize("seg", [False, True])
 def test_uniform_tiles(seg):
     """Long runs ("v v 9" tokens over whole tiles: the uniform-tile path of rle_device.h
