@@ -641,6 +641,13 @@ def run_rank(args):
         loop.graphs.clear()
     eager = other if loop.plain else None
     graphed = other if not loop.plain else None
+    # the headline is the faster of the two issue forms of the same K steps (the
+    # graph replay was ~2 % slower than eager issue on every round-5 box, ~1 % faster on others)
+    primary = {"value": total_u * args.steps / elapsed / GIB, "ms_per_step": elapsed / args.steps * 1e3}
+    use_other = other is not None and other["value"] > primary["value"]
+    if use_other:
+        elapsed = other["ms_per_step"] * 1e-3 * args.steps
+    headline_graph = loop.plain != use_other
 
     kern = roofline = conc = north = cpu = None
     if not dry:
@@ -655,7 +662,7 @@ def run_rank(args):
             cpu = cpu_leg(wl, args, c_bytes)
 
     if rank == 0:
-        value = total_u * args.steps / elapsed / GIB
+        value = other["value"] if use_other else total_u * args.steps / elapsed / GIB
         par = f"shard round-robin over {world} GPU(s)"
         if xch is not None:
             par += {"inline": ", RCCL all-gather of sizes + scan, one library call per step on the codec stream",
@@ -673,12 +680,13 @@ def run_rank(args):
                           "u_bytes_per_gpu": total_u // world, "c_bytes_rank0": c_bytes, "parallelism": par},
                "verified_bit_exact_roundtrip": ok, "host_wait": sched,
                "issue": ("one HIP graph of the K timed steps (captured before the timed region), replayed"
-                         if loop.plain else "eager: 2 launches per step from the host"),
+                         if headline_graph else "eager: 2 launches per step from the host")
+                        + " (the faster of the two issue forms, each timed over the same K steps)",
                "timed_region_events": timed_ev,
-               "value_eager": eager["value"] if eager else (round(value, 3) if not loop.plain else None),
-               "ms_per_step_eager": eager["ms_per_step"] if eager else None,
-               "value_graph": graphed["value"] if graphed else (round(value, 3) if loop.plain else None),
-               "ms_per_step_graph": graphed["ms_per_step"] if graphed else None,
+               "value_eager": eager["value"] if eager else (round(primary["value"], 3) if not loop.plain else None),
+               "ms_per_step_eager": eager["ms_per_step"] if eager else (round(primary["ms_per_step"], 4) if not loop.plain else None),
+               "value_graph": graphed["value"] if graphed else (round(primary["value"], 3) if loop.plain else None),
+               "ms_per_step_graph": graphed["ms_per_step"] if graphed else (round(primary["ms_per_step"], 4) if loop.plain else None),
                "kernels": kern, "roofline": roofline,
                "cpu_baseline": cpu, "north_star_dec64k": north, "concurrent_streams": conc}
         if xch is not None:

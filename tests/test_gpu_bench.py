@@ -1,7 +1,7 @@
 """bench.py at one rank on the GPU (the driver's N = 1 run, shortened): the timed loop issues the K
 steps eagerly (the default since round 6) or replays them from one HIP graph (RLE_BENCH_GRAPH=1), the
 round trip is verified, the other issue form is timed beside it (value_eager and value_graph both
-in the line), and the per-kernel split of the timed loop's GPU time stays below the step time
+in the line, `value` the faster of them), and the per-kernel split of the timed loop's GPU time stays below the step time
 (VERDICT r3 item 5)."""
 import json
 import os
@@ -24,7 +24,7 @@ def test_bench_one_rank(graph):
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["verified_bit_exact_roundtrip"] is True
-    assert ("graph" in out["issue"]) is (graph == "1"), out["issue"]
+    assert out["value"] == max(out["value_eager"], out["value_graph"]), out
     assert out["kernels"]["roundtrip"]["us"] <= out["ms_per_step"] * 1000 * 1.02, (out["kernels"], out["ms_per_step"])
     assert out["value_eager"] > 0 and out["value_graph"] > 0, out
-    assert out["value"] == (out["value_graph"] if graph == "1" else out["value_eager"]), out
+    assert ("graph" in out["issue"].split("(")[0]) is (out["value_graph"] > out["value_eager"]), out["issue"]
