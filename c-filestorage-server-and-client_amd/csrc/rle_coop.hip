@@ -29,9 +29,6 @@
 
 #include <atomic>
 
-#ifndef RLE_VARIANTS
-#define RLE_VARIANTS 0
-#endif
 
 namespace rle {
 

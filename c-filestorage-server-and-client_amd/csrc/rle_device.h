@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rle_build.h"
 #include "rle_mi355x.h"
 
 namespace rle {
@@ -145,15 +146,9 @@ __device__ __forceinline__ u32 lds_addr(const void* p) {
 }
 // Loads and stores in asm: hipcc neither counts nor waits for them; vm_wait() is the only wait
 // for them.  Loads go straight to LDS (LDS-DMA: lane i's 16 bytes land at lds + 16 i), so no
-// VGPR is in flight that the compiler could copy or reuse before the data lands.
-#ifndef RLE_LD_NT   // 1: the tile loads carry the non-temporal hint (streamed input: experiment)
-#define RLE_LD_NT 0
-#endif
-#if RLE_LD_NT
-#define RLE_LD_BITS " nt"
-#else
-#define RLE_LD_BITS ""
-#endif
+// VGPR is in flight that the compiler could copy or reuse before the data lands.  (The non-
+// temporal hint on the tile loads and on the large launches' stores measured slower everywhere,
+// r3n: DESIGN.md §4.)
 template <bool kStream = false>
 __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
     u32 keep;
@@ -163,7 +158,7 @@ __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
             "s_mov_b32 m0, %2\n\t"
             "s_waitcnt lgkmcnt(0)\n\t"   // earlier ds_reads of this slot have completed
             "s_nop 0\n\t"
-            "buffer_load_dwordx4 %1, %3, 0 offen" RLE_LD_BITS " lds\n\t"
+            "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "v"(voff), "s"(lds), "s"(rs)
@@ -180,25 +175,13 @@ __device__ __forceinline__ void dma_tile(u32x4 rs, u32 voff, u32 lds) {
             : "v"(voff), "s"(lds), "s"(rs)
             : "memory");
 }
-#ifndef RLE_NOSTORE
-#define RLE_NOSTORE 0
-#endif
 // Output stores.  wt (wave-uniform): write through (sc1: the line leaves the XCD's L2 and is not
 // kept dirty there).  A launch whose whole output fits in L2 otherwise ends with all of it dirty,
 // and the kernel boundary writes it back at about 6 TB/s (MI355X_MICROARCH.md, kernel boundaries):
 // 2.8 us for configs[1]'s 16.8 MB of decoded output.  Large launches store plainly, where writing
 // through measured 6-14 % slower (the launchers choose; rle_kernels.hip).
-#ifndef RLE_WT_BITS   // cache-policy bits of the write-through stores (experiments: "sc1 nt", "sc0 sc1")
-#define RLE_WT_BITS "sc1"
-#endif
-#ifndef RLE_ST_NT   // 1: the large launches' (write-back) stores carry the non-temporal hint (experiment)
-#define RLE_ST_NT 0
-#endif
-#if RLE_ST_NT
-#define RLE_WB_BITS " nt"
-#else
+#define RLE_WT_BITS "sc1"   // cache-policy bits of the write-through stores
 #define RLE_WB_BITS ""
-#endif
 __device__ __forceinline__ void vstore(u32x4 rs, u32 voff, u32x4 v, bool wt) {
     if (wt)
         asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen " RLE_WT_BITS "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
@@ -229,7 +212,7 @@ __device__ __forceinline__ void vm_wait(u32 n) {
     }
 }
 #undef RLE_VMW
-// the same for the deeper walks (walk_ring), whose counts reach past 15
+// the same for the walks whose counts reach past 15 (enc_stream_body)
 #define RLE_VMW2(N)                                           \
     case N:                                                   \
         asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
@@ -324,22 +307,6 @@ __device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
     // Loads are all consumed by the last step, so only a walk that stops early (~0u) drains.
     if (!primed) walk_prime<kStep, kLook>(rs, start, ntiles, lane, slots);
     u32 p1 = 0, p2 = 0;   // stores of the last step and of the one before
-#ifndef RLE_WALK_ROLLED   // 1: one copy of the step (slot chosen per tile) instead of two (code size)
-#define RLE_WALK_ROLLED 0
-#endif
-    if (RLE_WALK_ROLLED) {
-        for (u32 t = 0; t < ntiles; ++t) {
-            const u32 odd = t & 1u;
-            vm_wait(p2 + (t + 1u < ntiles ? kLoads : 0u) + p1);
-            p2 = p1;
-            p1 = step(t, slots + odd * kStride, Refill{rs, (t + 2u) * kStep + lo, odd ? l1 : l0, t + 2u < ntiles, look});
-            if (p1 == ~0u) {
-                vm_drain();
-                return true;
-            }
-        }
-        return false;
-    }
     for (u32 t = 0; t < ntiles; t += 2) {
         vm_wait(p2 + (t + 1u < ntiles ? kLoads : 0u) + p1);
         p2 = p1;
@@ -356,50 +323,6 @@ __device__ __forceinline__ bool walk_tiles(u32x4 rs, u32 start, u32 ntiles, u32 
             vm_drain();
             return true;
         }
-    }
-    return false;
-}
-// A deeper form of walk_tiles (decode tiles only, no lookahead load): kDepth slots, tile t in slot
-// t % kDepth, tile t + kDepth loaded into it by step t's next().  Vector-memory ops complete in
-// issue order, so the wait for tile t (loaded in step t - kDepth, before that step's stores) also
-// waits for every store issued before it: with two slots a step's stores must be acknowledged two
-// steps later, which output-heavy tiles (a 1008-byte tile of zero-filled data stores 3 KB in a few
-// hundred cycles) reach before the stores' latency has passed.  More slots give them more steps.
-// The ops issued after tile t's load: stores(t - D) and, for each step j in (t - D, t), the load of
-// tile j + D (when it exists) and stores(j) (steps j < 0 are the priming loads, without stores).
-template <u32 kDepth>
-__device__ __forceinline__ void walk_ring_prime(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots) {
-    const u32 lo = start + 16u * lane;
-    const u32 l0 = uniform(lds_addr(slots));
-    asm volatile("s_nop 4" ::: "memory");   // descriptor words may be fresh
-#pragma unroll
-    for (u32 d = 0; d < kDepth; ++d)
-        if (d < ntiles) Refill{rs, d * kTileStep + lo, l0 + d * kSlot, true, false}();
-}
-template <u32 kDepth, class Step>
-__device__ __forceinline__ bool walk_ring(u32x4 rs, u32 start, u32 ntiles, u32 lane, const uint8_t* slots, Step step) {
-    static_assert(kDepth >= 2u && kDepth <= 8u, "ring depth");
-    const u32 lo = start + 16u * lane;
-    const u32 l0 = uniform(lds_addr(slots));
-    u32 ps[kDepth];   // ps[k]: stores of step t - 1 - k
-#pragma unroll
-    for (u32 k = 0; k < kDepth; ++k) ps[k] = 0u;
-    u32 slot = 0;
-    for (u32 t = 0; t < ntiles; ++t) {
-        u32 nout = ps[kDepth - 1u];   // stores(t - D)
-#pragma unroll
-        for (u32 k = 0; k + 1u < kDepth; ++k)   // step j = t - 1 - k: its load of tile j + D, its stores
-            nout += ps[k] + (t - 1u - k + kDepth < ntiles ? 1u : 0u);
-        vm_wait_deep(nout);
-#pragma unroll
-        for (u32 k = kDepth - 1u; k > 0u; --k) ps[k] = ps[k - 1u];
-        const u32 ls = uniform(l0 + slot * kSlot);
-        ps[0] = step(t, slots + slot * kSlot, Refill{rs, (t + kDepth) * kTileStep + lo, ls, t + kDepth < ntiles, false});
-        if (ps[0] == ~0u) {
-            vm_drain();
-            return true;
-        }
-        slot = slot + 1u == kDepth ? 0u : slot + 1u;
     }
     return false;
 }
@@ -423,6 +346,14 @@ __device__ __forceinline__ u32 pkmax_lo2hi(u32 a) {
     return __builtin_bit_cast(u32, __builtin_elementwise_max(av, __builtin_shufflevector(av, av, 0, 0)));
 }
 
+// ---------------------------------------------------------------- diagnostic builds
+// Ablation builds (timing only, wrong output; never the product library), decode: 1 no phase scan,
+// 2 no scatter, 4 no fill, 8 scatter without its LDS writes, 16 no count-digit validation (still
+// exact on encoder output), 32 no uniform-tile test, 64 no flush stores; 128 (both kernels, in
+// rle_kernels.hip) no tiles walked at all (the fixed per-buffer cost).
+#ifndef RLE_ABL
+#define RLE_ABL 0
+#endif
 // ---------------------------------------------------------------- diagnostic stamps
 // RLE_STAMPS=1 builds (never the product library) sum s_memtime cycles per decode segment in
 // each wave and add them into g_stamps; rle_mi355x_stamps() reads the sums.  Read shares only:
@@ -665,9 +596,6 @@ __device__ __forceinline__ void enc_pass1(const u32* w, u32 T, u32 P, u32 NS, u3
 // may reach one byte past the tile's output, which the next tile rewrites (that byte is the next
 // tile's first output: a lane outputs 15 bytes only when its position 15 starts a token that
 // does not continue, so the next tile starts a token).  No staging, no pass 2.
-#ifndef RLE_ENC_FAST
-#define RLE_ENC_FAST 1
-#endif
 // Insertion selectors: entry i (the output index of an inserted '2', 0 = none), dword q: the
 // v_perm selector taking output bytes 4q..4q+3 from (S[q] : S[q-1] with bytes 0, 1 = '2').  Two
 // insertions are two passes.  6 dwords per entry (5 used): 8-byte aligned reads.  Each wave
@@ -890,7 +818,7 @@ template <bool k64, bool kFast = false>
 __device__ __forceinline__ u32 enc_tile_an(EncAn an, const uint2 look, u32 pos, u32 Ud, u32 Uo, u32 lane,
                                            uint8_t* stage, uint8_t* dst, u32x4 rso, EncState& st, const EncK& kc,
                                            const u32* elut) {
-    if (kFast && RLE_ENC_FAST && !st.head) {
+    if (kFast && !st.head) {
         if (pos + (k64 ? kEncStep : kTileStep) < Uo) {
             u32 r = enc_tile_run<k64>(an, pos, lane, stage, rso, st);
             if (r != kNotFast) return r;
@@ -1015,9 +943,6 @@ __device__ __forceinline__ u32 max_u(u32 a, u32 b) { return a > b ? a : b; }
 //  * literal pair: both tiles literal (enc_tile_fast's conditions), the second possibly the
 //    buffer's last tile (kTail1: its stores clipped at C, its last dword stored again).
 // Anything else runs the two tiles one after the other from their analyses (enc_tile_an).
-#ifndef RLE_ENC_PAIR   // 0: one tile per step (the walk of round 2)
-#define RLE_ENC_PAIR 1
-#endif
 // literal output of one tile: the lane's bytes with the '2's inserted (enc_tile_fast's body)
 struct EncLit {
     u32 out[5];
@@ -1052,9 +977,6 @@ __device__ __forceinline__ bool enc_lit_reject(const EncAn& a, u32 vm) {
 // starts).  With no run longer than 2, p15_l = del0_{l+1}, so the sum over the lanes before l
 // telescopes: exclusive offset 16 l + del0_l - del0_0 + (pairs of the lanes before l, two ballots
 // counted with v_mbcnt); the tile's total from the same ballots, p15_63 from lane 63's lookahead.
-#ifndef RLE_ENC_MBCNT
-#define RLE_ENC_MBCNT 1
-#endif
 __device__ __forceinline__ u32 mbcnt64(uint64_t b) {
     return __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
 }
@@ -1124,7 +1046,7 @@ __device__ __forceinline__ u32 enc_pair(const uint8_t* slotA, const uint8_t* slo
     const EncAn a0 = enc_analyze_bounds<true>(curA, lookA, pos, U, U, lane, st.prev_top, kc);
     // the byte before tile 1: tile 0's last byte (lane 63's top), from the data
     const EncAn a1 = enc_analyze_bounds<true>(curB, lookB, pos1, U, U, lane, readlane(curA.w & 0xFF000000u, 63), kc);
-    if (kFast && RLE_ENC_FAST && !st.head) {
+    if (kFast && !st.head) {
         const bool last1 = pos1 + kEncStep >= U;   // tile 1 is the buffer's last tile
         // run pair: both tiles one run (tile 1's first byte continues tile 0's last)
         if (!last1) {
@@ -1148,7 +1070,7 @@ __device__ __forceinline__ u32 enc_pair(const uint8_t* slotA, const uint8_t* slo
             u32 P0, P1;
             const u32 n0 = enc_lit_count(a0, 0xFFFFu, P0), n1 = enc_lit_count(a1, vm1, P1);
             u32 oi0, oi1, t0, t1;   // (exclusive offsets, totals)
-            if (RLE_ENC_MBCNT && pos1 + kEncStep <= U) {   // both tiles whole
+            if (pos1 + kEncStep <= U) {   // both tiles whole
                 enc_lit_offsets(a0, P0, lane, oi0, t0);
                 enc_lit_offsets(a1, P1, lane, oi1, t1);
             } else {
@@ -1248,9 +1170,6 @@ __device__ __forceinline__ bool walk_pairs(u32x4 rs, u32 start, u32 ntiles, u32 
 }
 
 // ================================================================ DECODE
-#ifndef RLE_ABL   // ablation builds (timing only, wrong output): 1 no phase scan, 2 no scatter, 4 no fill, 8 scatter without its LDS writes
-#define RLE_ABL 0     // (16: no count-digit validation -- still exact on encoder output; 32: no uniform-tile test)
-#endif
 // Token-phase table, indexed by an 8-bit mask n of "byte j differs from byte j+1" (the complement
 // of the 3-byte-token mask) and entry offset d (the first token start in the group, 0..2):
 // .x byte d = token-start mask, .y byte d = offset of the first start past the group (.y byte 3
@@ -1316,45 +1235,23 @@ struct DecState {
     u32 prev;      // stream byte before the current tile, in bits 24..31
     bool wt;       // write-through output stores (vstore)
     Stamps sp;     // diagnostic builds only
-    u32 lit_skip = 0;   // tiles left before the literal path is tried again (RLE_DEC_LITSKIP)
-    u32 vrun = 0;       // RLE_DEC_VRUN: 0x100 | v while the staged partial chunk is all v and staging
+    u32 vrun = 0;       // 0x100 | v while the staged partial chunk is all v and staging
                         // chunk 1 holds exactly one key, kv at position 0 (after a single-value tile)
     bool sv = false;    // the last tile was single-value (dec_fill_run): the next tries the uniform test
-    bool hold_ok = false;   // RLE_DEC_HOLD in this kernel (the one-wave decode only)
-    u32 vhold = 0;          // chunks of st.fillc after `flushed` held back to a 128-byte line (dec_release)
 };
 
-// Bank spread of the decode staging (RLE_SWZ).  Unswizzled, a random-data tile decodes 16 positions
-// (32 B of keys) per lane, so the lanes of one scatter write sit 32 B apart and 8 of every 32-lane
-// group share a bank.  Mode 1: dword i of the 32-B chunk at A lives at A + 4 (i ^ g), g = bits 7..9
-// of A (flush reads dword by dword).  Mode 2: the 16-B slot s of the 128-B row at A lives at slot
-// s ^ g, g = bits 7..9 of A, so the lanes 128 B apart land in 8 different slots and the flush still
-// reads each 16-B half of a chunk with one ds_read_b128.  Every staging access goes through sswz;
-// the staging is 128-B aligned, so a row never leaves it.
-#ifndef RLE_SWZ
-#define RLE_SWZ 0
-#endif
-__device__ __forceinline__ u32 sswz(u32 t) {
-    if (RLE_SWZ == 1) return bitop3<0xF0 ^ (0xCC & 0xAA)>(t, t >> 5, 0x1Cu);
-    if (RLE_SWZ == 2) return bitop3<0xF0 ^ (0xCC & 0xAA)>(t, t >> 3, 0x70u);
-    return t;
-}
+// Staging address of a position's key.  Unswizzled, a random-data tile decodes 16 positions (32 B
+// of keys) per lane, so the lanes of one scatter write sit 32 B apart and 8 of every 32-lane group
+// share a bank; two XOR swizzles of the chunks over a 128-B row (dword-wise, 16-B-slot-wise) cut the
+// conflicts but measured slower (runs50 +8 %, runs90 +5 %, r5p), so the staging is
+// addressed linearly.  Every staging access still goes through sswz.
+__device__ __forceinline__ u32 sswz(u32 t) { return t; }
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-// One 32-byte staging chunk (16 u16 keys) at s4, through the staging swizzle.
+// One 32-byte staging chunk (16 u16 keys) at s4.
 __device__ __forceinline__ void dec_read_chunk(const u32x4* s4, u32x4& a, u32x4& b) {
-    if (RLE_SWZ == 1) {
-        const u32 Ag = sswz(lds_addr(s4));   // dword m of the chunk sits at Ag ^ 4 m
-        auto rd = [&](u32 m) { return *reinterpret_cast<const __attribute__((address_space(3))) u32*>(Ag ^ (4u * m)); };
-        a = u32x4{rd(0), rd(1), rd(2), rd(3)};
-        b = u32x4{rd(4), rd(5), rd(6), rd(7)};
-    } else if (RLE_SWZ == 2) {
-        a = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4)));
-        b = *reinterpret_cast<const lds_u32x4*>(sswz(lds_addr(s4) + 16u));
-    } else {
-        a = s4[0];
-        b = s4[1];
-    }
+    a = s4[0];
+    b = s4[1];
 }
 
 // The flush's fill of one 32-byte staging chunk (16 u16 keys a, b): the position index p goes into
@@ -1363,24 +1260,14 @@ __device__ __forceinline__ void dec_read_chunk(const u32x4* s4, u32x4& a, u32x4&
 __device__ __forceinline__ void dec_fill_scan(u32x4 a, u32x4 b, u32 (&L)[8]) {
     L[0] = a.x | 0x01000000u; L[1] = a.y | 0x03000200u; L[2] = a.z | 0x05000400u; L[3] = a.w | 0x07000600u;
     L[4] = b.x | 0x09000800u; L[5] = b.y | 0x0B000A00u; L[6] = b.z | 0x0D000C00u; L[7] = b.w | 0x0F000E00u;
-#ifndef RLE_FILL_OPSEL   // 1: the scan in 15 op_sel max instructions (0: round 2's 23, with v_perm)
-#define RLE_FILL_OPSEL 1
-#endif
-    if (RLE_FILL_OPSEL && !(RLE_ABL & 4)) {
-        // prefix max inside each dword (position 2m+1 takes 2m), then along the chunk: dword m takes
-        // the high half (position 2m-1, the prefix so far) of dword m-1 in both halves
+    // 15 op_sel max instructions (round 3; round 2's form took 23 with v_perm): prefix max inside
+    // each dword (position 2m+1 takes 2m), then along the chunk: dword m takes the high half
+    // (position 2m-1, the prefix so far) of dword m-1 in both halves
+    if (!(RLE_ABL & 4)) {
 #pragma unroll
         for (u32 m = 0; m < 8; ++m) L[m] = pkmax_lo2hi(L[m]);
 #pragma unroll
         for (u32 m = 1; m < 8; ++m) L[m] = pkmax_bhi(L[m], L[m - 1]);
-    } else if (!(RLE_ABL & 4)) {
-        // running max of the even positions (low halves) and of the odd ones (high halves) ...
-#pragma unroll
-        for (u32 m = 1; m < 8; ++m) L[m] = pkmax(L[m], L[m - 1]);
-        // ... then position 2m takes the odd max up to 2m-1, position 2m+1 the even max up to 2m
-#pragma unroll
-        for (u32 m = 7; m > 0; --m) L[m] = pkmax(L[m], __builtin_amdgcn_perm(L[m], L[m - 1], 0x05040302u));
-        L[0] = pkmax(L[0], L[0] << 16);
     }
 }
 // The chunk's 16 output bytes: each position's latest key at or before it, else the byte `carry`
@@ -1399,21 +1286,15 @@ __device__ __forceinline__ u32x4 dec_fill_out_rep(const u32 (&L)[8], u32 crep) {
     return o;
 }
 
-#ifndef RLE_FILL_CREP   // 1: the carry moves as the chunk's whole last dword, spread by one v_perm
-#define RLE_FILL_CREP 1
-#endif
 // Store staged chunks 1..nfl (outputs [flushed, flushed + 16 nfl)) and re-zero them.
 __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* stage, u32x4 rso, u32 flushed, u32& fillc,
                                          u32& head, uint8_t* dst, Stamps& sp) {
     const u32 rounds = (nfl + kWave - 1u) / kWave;
     // the carry's fill halves (0x10 above the byte) in a VGPR, so the v_perm's selector can be the
     // one constant-bus operand (no per-round v_mov)
-    const u32 k10 = RLE_FILL_CREP && rounds ? vconst(0x10101010u) : 0u;
-#ifndef RLE_FLUSH_ZREG   // 1: the re-zeroing stores take a zero tuple held in VGPRs over the loop
-#define RLE_FLUSH_ZREG 1
-#endif
-    const u32x4 Z = RLE_FLUSH_ZREG && rounds ? u32x4{vconst(0u), vconst(0u), vconst(0u), vconst(0u)}
-                                             : u32x4{0u, 0u, 0u, 0u};
+    const u32 k10 = rounds ? vconst(0x10101010u) : 0u;
+    // the re-zeroing stores take a zero tuple held in VGPRs over the loop
+    const u32x4 Z = rounds ? u32x4{vconst(0u), vconst(0u), vconst(0u), vconst(0u)} : u32x4{0u, 0u, 0u, 0u};
     for (u32 k = 0; k < rounds; ++k) {
         const u32 c = k * kWave + lane;
         const bool active = c < nfl;
@@ -1430,20 +1311,14 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
         RLE_STAMP(sp, 3);   // flush: staging reads
         u32 L[8];
         dec_fill_scan(a, b, L);
-        // byte of the chunk's last key = its last output byte: bits 16..23 of L[7]
-        u32 lastb;
-        u32x4 o;
-        if (RLE_FILL_CREP) {
-            lastb = L[7];
-            const u32 prev = from_prev_lane(L[7], fillc << 16);
-            o = dec_fill_out_rep(L, __builtin_amdgcn_perm(prev, k10, 0x00060006u));
-        } else {
-            lastb = (L[7] >> 16) & 0xFFu;
-            o = dec_fill_out(L, from_prev_lane(lastb, fillc));
-        }
+        // byte of the chunk's last key = its last output byte: bits 16..23 of L[7]; the carry moves
+        // as the chunk's whole last dword, spread by one v_perm
+        const u32 lastb = L[7];
+        const u32 prev = from_prev_lane(L[7], fillc << 16);
+        const u32x4 o = dec_fill_out_rep(L, __builtin_amdgcn_perm(prev, k10, 0x00060006u));
         RLE_STAMP(sp, 4);   // flush: fill + carry
         const bool skip = head && c == 0u;   // shared with the previous segment: byte stores below
-        vstore(rso, (active && !skip && !RLE_NOSTORE) ? flushed + 16u * c : kOOB, o, wt);   // RLE_NOSTORE: diagnostic
+        vstore(rso, (active && !skip && !(RLE_ABL & 64)) ? flushed + 16u * c : kOOB, o, wt);   // (RLE_ABL 64: diagnostic)
         if (skip && active) {
             const u32 wv[4] = {o.x, o.y, o.z, o.w};
             for (u32 j = head; j < 16u; ++j) dst[flushed + j] = (uint8_t)(wv[j >> 2] >> (8u * (j & 3u)));
@@ -1451,16 +1326,11 @@ __device__ __forceinline__ u32 dec_flush(bool wt, u32 nfl, u32 lane, uint8_t* st
         head = 0;
         RLE_STAMP(sp, 5);   // flush: store issue
         if (active) {
-            if (RLE_SWZ == 2) {
-                *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(s4))) = u32x4{0u, 0u, 0u, 0u};
-                *reinterpret_cast<lds_u32x4*>(sswz(lds_addr(s4) + 16u)) = u32x4{0u, 0u, 0u, 0u};
-            } else {
-                s4[0] = Z;
-                s4[1] = Z;
-            }
+            s4[0] = Z;
+            s4[1] = Z;
         }
         const u32 lastlane = (nfl - 1u - k * kWave) < (kWave - 1u) ? (nfl - 1u - k * kWave) : (kWave - 1u);
-        fillc = RLE_FILL_CREP ? (readlane(lastb, lastlane) >> 16) & 0xFFu : readlane(lastb, lastlane);
+        fillc = (readlane(lastb, lastlane) >> 16) & 0xFFu;
         wave_lds_sync();
         RLE_STAMP(sp, 6);   // flush: re-zero + sync
     }
@@ -1539,13 +1409,9 @@ __device__ __forceinline__ DecPrep dec_prepare(const u32x4 cur, u32 pos, u32 C, 
     // values on lanes 0..62; lane 63's incl, which no consumer reads, is then its own map).  Streams
     // whose lanes keep the phase open (a run of one digit-like byte) take the scan.  As the encode
     // tile's run-start scan (enc_analyze_bounds).
-#ifndef RLE_DEC_MAPSKIP
-#define RLE_DEC_MAPSKIP 1
-#endif
     constexpr uint64_t kOwnedLanes = (1ull << kOwnLanes) - 1ull;
     if (RLE_ABL & 1) r.incl = map;
-    else if (RLE_DEC_MAPSKIP &&
-             !(__builtin_amdgcn_ballot_w64(map != __builtin_amdgcn_perm(map, map, 0x03000000u)) & kOwnedLanes))
+    else if (!(__builtin_amdgcn_ballot_w64(map != __builtin_amdgcn_perm(map, map, 0x03000000u)) & kOwnedLanes))
         r.incl = map;
     else r.incl = wave_scan_incl(map, kMapId, OpMap());
     r.excl = from_prev_lane(r.incl, kMapId);
@@ -1605,9 +1471,6 @@ __device__ __forceinline__ DecLen dec_lengths_t(const DecPrep& p, u32 d) {
         }
     }
     u32 bad = 0u, sum = 0u;
-#ifndef RLE_SCAT_NEXT   // 1 (round 4): interior positions of dwords 0..2 write at the next token's slot (dec_scatter)
-#define RLE_SCAT_NEXT 1
-#endif
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 P80 = bitop3<0xF0 & ~0xCC & 0xAA>(S80[k], p.g[k], VD80[k]);   // 3-byte start, digit in stream
@@ -1620,8 +1483,9 @@ __device__ __forceinline__ DecLen dec_lengths_t(const DecPrep& p, u32 d) {
         const u32 S01 = fshr<7>(S80[k]);
         r.S80[k] = S80[k];
         r.S01[k] = S01;
-        // (only dword 3 needs it with RLE_SCAT_NEXT: dec_scatter)
-        r.N02[k] = (RLE_SCAT_NEXT && k < 3u) ? 0u : fsub(O02[k], fshr<6>(S80[k]));
+        // (only dword 3 needs it: interior positions of dwords 0..2 write at the next token's slot,
+        // dec_scatter)
+        r.N02[k] = k < 3u ? 0u : fsub(O02[k], fshr<6>(S80[k]));
         r.W[k] = fadd(S01, b & P7F);
         sum = fadd(sum, r.W[k]);
     }
@@ -1635,23 +1499,20 @@ __device__ __forceinline__ DecLen dec_lengths(const DecPrep& p, u32 d) {
     return p.tail ? dec_lengths_t<true>(p, d) : dec_lengths_t<false>(p, d);
 }
 
-#ifndef RLE_SCAT_MASK   // 1: the scatter writes token starts only (interior writes exec-masked off)
-#define RLE_SCAT_MASK 0
-#endif
-#ifndef RLE_SCAT_D16HI   // 1: the odd positions' keys stored from the high halves (no shifts);
-#define RLE_SCAT_D16HI 0   // measured neutral (r3j: 64 KiB runs50 -0.6 %, runs90 +0.3 %), off
-#endif
 // The scatter of one lane's decoded positions into the staging (2 bytes per position): endk = the
 // staging byte address of the lane's first decoded position.  u16 per position: the byte, with
 // the start flag (0x80) as the high byte: 0x80vv at a token start, an unflagged 0x00vv (ignored by
 // the fill) anywhere else.  Where an interior position (a 3-byte token's second byte or count digit)
-// writes its unflagged key: RLE_SCAT_NEXT (round 4), positions 0..13 at the slot right after their
+// writes its unflagged key (round 4): positions 0..13 at the slot right after their
 // own token's output, which is the next token's start slot: that token starts in the same lane (a
 // token spans at most 3 positions), whose later write of the flagged key (program order) replaces
 // it; positions 14 and 15, whose next token may start in the next lane (written by an earlier
 // instruction there), keep round 3's rule: one slot back, their own token's last decoded position,
 // which never holds a key (counts are >= 2 on this path).  Saves the N02 / R arithmetic of three of
-// the four dwords.
+// the four dwords.  (Measured and not kept: exec-masking the interior writes off, so that only
+// token starts write, cut the bank conflicts by a third but cost 11-14 % more VALU and ran 10-12 %
+// slower, r5ad; storing the odd positions from the high halves with ds_write_b16_d16_hi was
+// neutral, r3j: DESIGN.md §4.)
 __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 endk) {
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
@@ -1666,24 +1527,10 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
             if (RLE_ABL & 8) asm volatile("" ::"v"(t), "v"(key));   // ablation: no LDS write
             else *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(t)) = (uint16_t)key;
         };
-        // the high u16 of key: ds_write_b16_d16_hi stores it without a shift (the compiler hoists
-        // the shifts out of the pass loop, where the d16_hi pattern no longer matches)
-        auto put_hi = [&put](u32 t, u32 key) {
-            if (RLE_SCAT_D16HI && !(RLE_ABL & 8))
-                asm volatile("ds_write_b16_d16_hi %0, %1" ::"v"(sswz(t)), "v"(key) : "memory");
-            else put(t, key >> 16);
-        };
-        if (RLE_SCAT_MASK) {   // token starts only: the interior writes' lanes leave the bank conflicts
-            if ((int)(xk_lo << 16) < 0) put(sub_byte<0>(endk, R), xk_lo);
-            if ((int)xk_lo < 0) put_hi(sub_byte<1>(endk, R), xk_lo);
-            if ((int)(xk_hi << 16) < 0) put(sub_byte<2>(endk, R), xk_hi);
-            if ((int)xk_hi < 0) put_hi(sub_byte<3>(endk, R), xk_hi);
-        } else {
-            put(sub_byte<0>(endk, R), xk_lo);
-            put_hi(sub_byte<1>(endk, R), xk_lo);
-            put(sub_byte<2>(endk, R), xk_hi);
-            put_hi(sub_byte<3>(endk, R), xk_hi);
-        }
+        put(sub_byte<0>(endk, R), xk_lo);
+        put(sub_byte<1>(endk, R), xk_lo >> 16);
+        put(sub_byte<2>(endk, R), xk_hi);
+        put(sub_byte<3>(endk, R), xk_hi >> 16);
     }
 }
 
@@ -1699,9 +1546,6 @@ __device__ __forceinline__ void dec_scatter(const DecLen& ln, const u32* w, u32 
 // twice are equal.  The last lane's store reaches <= 16 bytes past the tile's output; the next
 // tile's (or the finish's) stores, issued later by the same wave, overwrite them.  No staging, no
 // scatter, no fill: random and text-like data decode with about half the VALU work.
-#ifndef RLE_DEC_FAST
-#define RLE_DEC_FAST 1
-#endif
 // Compaction selectors: entry t (a deleted position, 16 = none), dword q: the v_perm selector
 // taking output bytes 4q..4q+3 from (y[q+1]:y[q]) once position t is removed.  A lane's two
 // deletions are two passes, the higher position first.  17 entries of 16 bytes: every wave
@@ -1747,60 +1591,36 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
     const u32 sa = __builtin_amdgcn_perm(0u, pr.ta.x, 0x0C0C0C00u | dl);
     const u32 sb = __builtin_amdgcn_perm(0u, pr.tb.x, 0x0C0C0C00u | mid);
     const u32 P16 = (sa | (sb << 8)) & ~NE16 & lim;   // pair starts (bits 0..15)
-#ifndef RLE_DEC_DIGIT2   // 1: the '2' test reads only the deleted digit bytes (round 3); 0: every position's digit
-#define RLE_DEC_DIGIT2 1
-#endif
     // deleted positions: digits of pairs started in this lane or (bits 14, 15) the lane before, and
     // in lane 0 the tile's first d positions; lane 63 keeps only a pair's second byte at position 0
     const u32 prevP = from_prev_lane(P16, 0u);
     const u32 dig = ((P16 << 2) | (prevP >> 14)) & lim;   // the digits
     const u32 del = lane == 0u ? dig | (lowmask(st.d) & lim) : dig;
-    bool reject;
-    if (RLE_DEC_DIGIT2) {
-        // every pair's count digit is '2': the digits are exactly the deleted positions other than
-        // lane 0's first d (the previous tile's token, checked there) -- on lane 63 only those of
-        // lane 62's pairs.  At most 2 per lane pass the limit below, so only those bytes are read
-        // (one v_perm pair each), not a '2' test of every position.
-        const u32 chk = lane < kOwnLanes ? dig : ((prevP >> 14) & 3u);
-        const u32 c1 = (u32)__builtin_ctz(chk | 0x10000u), c2 = (u32)__builtin_ctz((chk & (chk - 1u)) | 0x10000u);
-        auto byte_at = [&](u32 q) {   // byte q (0..15) of the lane's 16 bytes, in bits 0..7
-            const u32 lo = __builtin_amdgcn_perm(w[1], w[0], q & 7u), hi = __builtin_amdgcn_perm(w[3], w[2], q & 7u);
-            return (q & 8u) ? hi : lo;
-        };
-        const bool bad1 = c1 < 16u && (byte_at(c1) & 0xFFu) != 0x32u;
-        const bool bad2 = c2 < 16u && (byte_at(c2) & 0xFFu) != 0x32u;
-        // (lane 63's own pairs belong to the next tile: only its digit test counts, so the ballot
-        // below takes every lane)
-        reject = bad1 || bad2 || (lane < kOwnLanes && __builtin_popcount(del) > 2);
-        if (kTail) reject = reject || (lane < kOwnLanes && (P16 & ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2)) != 0u);
-    } else {
-        // every pair's count digit (position j + 2) is '2' (and, in a tail tile, lies below C)
-        const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
-                           alignbyte(pr.la, w[3], 2)};
-        u32 nz[4];
-#pragma unroll
-        for (u32 k = 0; k < 4; ++k) {
-            const u32 t = dg[k] ^ 0x32323232u;
-            nz[k] = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & kc.K7F), t, kc.K80);
-        }
-        const u32 za = __builtin_amdgcn_udot4(nz[1], kc.C2, __builtin_amdgcn_udot4(nz[0], kc.C1, 0u, false), false);
-        const u32 zb = __builtin_amdgcn_udot4(nz[3], kc.C2, __builtin_amdgcn_udot4(nz[2], kc.C1, 0u, false), false);
-        u32 NZ16 = (za >> 7) | (zb << 1);   // digit position j + 2 holds something other than '2'
-        if (kTail) NZ16 |= ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2);   // ... or lies past C
-        reject = (P16 & NZ16) != 0u || __builtin_popcount(del) > 2;
-    }
+    // every pair's count digit is '2': the digits are exactly the deleted positions other than lane
+    // 0's first d (the previous tile's token, checked there) -- on lane 63 only those of lane 62's
+    // pairs.  At most 2 per lane pass the limit below, so only those bytes are read (one v_perm pair
+    // each), not a '2' test of every position (round 3).
+    const u32 chk = lane < kOwnLanes ? dig : ((prevP >> 14) & 3u);
+    const u32 c1 = (u32)__builtin_ctz(chk | 0x10000u), c2 = (u32)__builtin_ctz((chk & (chk - 1u)) | 0x10000u);
+    auto byte_at = [&](u32 q) {   // byte q (0..15) of the lane's 16 bytes, in bits 0..7
+        const u32 lo = __builtin_amdgcn_perm(w[1], w[0], q & 7u), hi = __builtin_amdgcn_perm(w[3], w[2], q & 7u);
+        return (q & 8u) ? hi : lo;
+    };
+    const bool bad1 = c1 < 16u && (byte_at(c1) & 0xFFu) != 0x32u;
+    const bool bad2 = c2 < 16u && (byte_at(c2) & 0xFFu) != 0x32u;
+    // (lane 63's own pairs belong to the next tile: only its digit test counts, so the ballot below
+    // takes every lane)
+    bool reject = bad1 || bad2 || (lane < kOwnLanes && __builtin_popcount(del) > 2);
+    if (kTail) reject = reject || (lane < kOwnLanes && (P16 & ~(lowmask(pr.left < 18u ? pr.left : 18u) >> 2)) != 0u);
     const u32 K = lane < kOwnLanes ? (~del & lim) : ((prevP >> 15) & 1u);
     const u32 kept = (u32)__builtin_popcount(K);
     // Output offsets.  A whole tile's owned lanes keep 16 - d bytes, d = their deletions (<= 2, else
     // the tile is rejected below), and lane 63 keeps 0 or 1: so the exclusive offset of lane l is
     // 16 l less the deletions of the lanes before it, two ballots counted with v_mbcnt, and the
     // tile's total comes from the same ballots on the scalar unit -- no DPP scan on the tile's
-    // dependent chain (RLE_DEC_MBCNT, round 5).  Tail tiles (owned lanes cut short) take the scan.
-#ifndef RLE_DEC_MBCNT
-#define RLE_DEC_MBCNT 1
-#endif
+    // dependent chain (round 5).  Tail tiles (owned lanes cut short) take the scan.
     u32 oexcl, ttot;
-    if (RLE_DEC_MBCNT && !kTail) {
+    if (!kTail) {
         const u32 d = lane < kOwnLanes ? (u32)__builtin_popcount(del) : 0u;
         const uint64_t B1 = __builtin_amdgcn_ballot_w64(d >= 1u), B2 = __builtin_amdgcn_ballot_w64(d >= 2u);
         const uint64_t B3 = __builtin_amdgcn_ballot_w64(lane == kWave - 1u && kept != 0u);
@@ -1813,7 +1633,7 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
         ttot = readlane(oincl, kWave - 1u);
         oexcl = oincl - kept;
     }
-    if (__builtin_amdgcn_ballot_w64(reject) & (RLE_DEC_DIGIT2 ? ~0ull : kOwned)) return kNotFast;
+    if (__builtin_amdgcn_ballot_w64(reject)) return kNotFast;
     if (kTail ? (ttot < 4u || st.out_pos + ttot > U) : st.out_pos + ttot + 16u > U) return kNotFast;
     if (kTail) {
         rso.z = uniform(st.out_pos + ttot);   // clip every store of this tile at its output end
@@ -1882,44 +1702,17 @@ __device__ __forceinline__ u32 dec_tile_fast(const DecPrep& pr, u32 lane, const 
 }
 
 // Single-value tile (dec_tile): ttot copies of v after the staged partial chunk.  The caller sets
-// the tile's exit state (st.d, st.prev).
-#ifndef RLE_DEC_ALIGN   // 1: single-value tiles' stores start on 128-byte lines (dec_fill_run)
-#define RLE_DEC_ALIGN 0
-#endif
-#ifndef RLE_DEC_VRUN   // 1: consecutive single-value tiles of one byte skip the staging (st.vrun)
-#define RLE_DEC_VRUN 1
-#endif
-#ifndef RLE_DEC_HOLD   // 1: single-value tiles store up to a 128-byte line and hold back the rest (st.vhold)
-#define RLE_DEC_HOLD 0
-#endif
-// Store the chunks a single-value tile held back (st.vhold of them, all st.fillc), before any path
-// that stages from `flushed`.  Held chunks exist only while st.vrun says the staged partial chunk is
-// all st.fillc too, so afterwards staging chunk 1 is that partial chunk again.  Returns the store
-// instructions issued (0 or 1).
-__device__ __forceinline__ u32 dec_release(u32 lane, u32x4 rso, DecState& st) {
-    if (!RLE_DEC_HOLD || st.vhold == 0u) return 0u;
-    const u32 vv = rep4(st.fillc);
-    vstore(rso, lane < st.vhold ? st.flushed + 16u * lane : kOOB, u32x4{vv, vv, vv, vv}, st.wt);
-    st.flushed += 16u * st.vhold;
-    st.vhold = 0u;
-    return 1u;
-}
+// the tile's exit state (st.d, st.prev).  Measured and not kept (r5ar): stores
+// shifted onto 128-byte lines, and holding back the chunks past the last line so that no line is
+// written in two halves by two tiles: within 0.3 % on dec64k, +2 % on configs[1].
 __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st) {
     // the previous tile was single-value tile of the same byte that left staging chunk 1 as one key
-    // kv at position 0: the staged positions are all v, so chunk 0 is rep4(v) without reading or
-    // filling the staging, and the staging stays as it is when this tile leaves a partial chunk too
-    // (held-back chunks, st.vhold, are all v as well and are simply stored with this tile's)
-    const bool known = RLE_DEC_VRUN && st.vrun == (0x100u | v);
-    const u32 pre = known ? 0u : dec_release(lane, rso, st);
-    const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl_all = total >> 4;
+    // kv at position 0 (st.vrun): the staged positions are all v, so chunk 0 is rep4(v) without
+    // reading or filling the staging, and the staging stays as it is when this tile leaves a partial
+    // chunk too
+    const bool known = st.vrun == (0x100u | v);
+    const u32 rel0 = st.out_pos - st.flushed, total = rel0 + ttot, nfl = total >> 4;
     const u32 vv = rep4(v);
-    // RLE_DEC_HOLD: when this tile leaves a partial chunk of v (the state stays known), store only up
-    // to the last 128-byte line boundary: the next tile's stores then start on a line, so no line is
-    // written in two halves by two tiles (the pattern kernel: -3 %, profiles/r5ap_*)
-    const u32 hold = RLE_DEC_HOLD && st.hold_ok && RLE_DEC_VRUN && nfl_all != 0u && (total & 15u) != 0u
-                         ? ((rso.x >> 4) + (st.flushed >> 4) + nfl_all) & 7u : 0u;
-    const u32 nfl = nfl_all - (known || hold < nfl_all ? hold : 0u);   // (unknown: chunk 0 mixes staged keys)
-    const u32 held = nfl_all - nfl;
     u32 c0[4] = {vv, vv, vv, vv};
     if (!known) {
         // chunk 0: the staged positions [0, rel0) filled like a flush, then v (every lane computes it)
@@ -1936,23 +1729,19 @@ __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* 
             c0[k] = (fv[k] & m) | (vv & ~m);
         }
     }
-    // RLE_DEC_ALIGN: lane l of store k takes chunk 64 k + l - r, r = the chunks between the last
-    // 128-byte line start and the first store address, so every store instruction covers whole
-    // lines (8 for 64 lanes, not 9); an extra store when nfl + r passes a multiple of 64
-    const u32 r = RLE_DEC_ALIGN ? ((rso.x >> 4) + (st.flushed >> 4)) & 7u : 0u;
-    const u32 rounds = (nfl + r + kWave - 1u) / kWave;
+    const u32 rounds = (nfl + kWave - 1u) / kWave;
     for (u32 k = 0; k < rounds; ++k) {
-        const u32 c = k * kWave + lane - r;   // (wraps past nfl for the r lanes before chunk 0)
+        const u32 c = k * kWave + lane;
         const u32x4 o = c == 0u ? u32x4{c0[0], c0[1], c0[2], c0[3]} : u32x4{vv, vv, vv, vv};
         vstore(rso, c < nfl ? st.flushed + 16u * c : kOOB, o, st.wt);
     }
-    if (!(known && nfl_all != 0u && (total & 15u) != 0u)) {
+    if (!(known && nfl != 0u && (total & 15u) != 0u)) {
         wave_lds_sync();   // every lane has read staging chunk 1
         // staging chunk 1 = the new partial chunk: the old keys plus a key at rel0 (nothing flushed),
         // else a key at position 0 (when anything is left) and zeros
         const u32 kv = kKeyFlag | v;
         if (lane == 0u) {
-            if (nfl_all == 0u) {
+            if (nfl == 0u) {
                 *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(sswz(lds_addr(stage) + 32u + 2u * rel0)) = (uint16_t)kv;
             } else {
                 const u32 k0 = (total & 15u) ? kv : 0u;
@@ -1962,13 +1751,12 @@ __device__ __forceinline__ u32 dec_fill_run(u32 v, u32 ttot, u32 lane, uint8_t* 
         }
         wave_lds_sync();
     }
-    st.vrun = (nfl_all != 0u && (total & 15u) != 0u) ? (0x100u | v) : 0u;
+    st.vrun = (nfl != 0u && (total & 15u) != 0u) ? (0x100u | v) : 0u;
     st.sv = true;
     st.fillc = v;
     st.flushed += 16u * nfl;
-    st.vhold = held;
     st.out_pos += ttot;
-    return rounds + pre;
+    return rounds;
 }
 __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t* stage, u32x4 rso, DecState& st,
                                              const DecPrep& pr) {
@@ -1988,9 +1776,6 @@ __device__ __forceinline__ u32 dec_tile_fill(u32 v, u32 ttot, u32 lane, uint8_t*
 // unit, then every owned byte and the lookahead bytes its last token reads (lane 63's first d) on
 // the vector unit, so other tiles pay a few scalar instructions.  Byte-identical to the general
 // path: the same tokens, each 3 bytes long (its first two bytes are equal) with count 9.
-#ifndef RLE_DEC_UNIFORM   // 0: no uniform-tile test in any kernel (A/B builds)
-#define RLE_DEC_UNIFORM 1
-#endif
 constexpr u32 kUniformOut = 9u * (kTileStep / 3u);   // 3024
 __device__ __forceinline__ u32 uniform_pat(u32 m, u32 vv) {
     return m == 0u ? ((vv & 0xFF00FFFFu) | 0x00390000u)
@@ -2028,9 +1813,7 @@ template <bool kFast = false, u32 kChunks = kDecChunks>
 __device__ __forceinline__ u32 dec_tile_pr(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
                                            uint8_t* stage, uint8_t* dst, u32x4 rso, DecState& st, const DecK& kc,
                                            const u32x4* clut) {
-    const u32 rel = dec_release(lane, rso, st);   // (RLE_DEC_HOLD: every path below stages from `flushed`)
-    const u32 r = dec_tile_pr_body<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
-    return r == ~0u ? r : r + rel;
+    return dec_tile_pr_body<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
 }
 template <bool kFast, u32 kChunks>
 __device__ __forceinline__ u32 dec_tile_pr_body(const DecPrep& pr, u32 pos, u32 C, u32 Co, u32 U, u32 lane,
@@ -2039,30 +1822,18 @@ __device__ __forceinline__ u32 dec_tile_pr_body(const DecPrep& pr, u32 pos, u32 
     // Segments (Co < C; rle_segmented.hip) end on tile edges, so their last tile (a tail tile) is a
     // whole tile whose tail form clips its stores at its output end: the next segment's output is
     // another wave's.  A segment's first tile takes the literal path when nothing is staged yet (its
-    // stores start at the segment's output offset, never before it).  RLE_DEC_SEGFAST=0: neither
-    // (round 2's rule: no literal path on a segment's first or last tile).
-#ifndef RLE_DEC_SEGFAST
-#define RLE_DEC_SEGFAST 1
-#endif
+    // stores start at the segment's output offset, never before it).  (Round 2 kept the literal path
+    // off a segment's first and last tile.)
     const u32 vrun = st.vrun;   // (the single-value path below keeps it; every other path changes the staging)
     st.vrun = 0u;
     st.sv = false;   // (dec_fill_run sets it again on the single-value path)
-    const bool head_ok = !st.head || (RLE_DEC_SEGFAST && st.out_pos - st.flushed == st.head);
-    // RLE_DEC_LITSKIP > 0: a tile that fails the literal path's test makes the next that many tiles
-    // skip it (round-4 experiment): run-heavy data (runs50 / runs90) fails it on every tile, paying
-    // its reject test (~7 VALU and ~10 SALU) for nothing.
-#ifndef RLE_DEC_LITSKIP   // 0 (off): measured r4a, same process: runs50 -1 %, but configs[1] decode +8 %
-#define RLE_DEC_LITSKIP 0     // and 64 KiB random +2 % (the extra loop state changes the code)
-#endif
-    if (kFast && RLE_DEC_FAST && head_ok && (!pr.tail || Co == C || RLE_DEC_SEGFAST)) {
-        if (RLE_DEC_LITSKIP && st.lit_skip && !pr.tail) {
-            --st.lit_skip;
-        } else {
-            const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
-                                  : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
-            if (r != kNotFast) return r;
-            st.lit_skip = RLE_DEC_LITSKIP;
-        }
+    const bool head_ok = !st.head || st.out_pos - st.flushed == st.head;
+    // (Skipping the literal test for a few tiles after a failed one, round 4: runs50 -1 %, but
+    // configs[1] decode +8 % and 64 KiB random +2 %; not kept.)
+    if (kFast && head_ok) {
+        const u32 r = pr.tail ? dec_tile_fast<true>(pr, lane, clut, stage, rso, U, st, kc)
+                              : dec_tile_fast<false>(pr, lane, clut, stage, rso, U, st, kc);
+        if (r != kNotFast) return r;
     }
     const DecLen ln = dec_lengths(pr, st.d);
     const u32* w = pr.w;
@@ -2084,7 +1855,7 @@ __device__ __forceinline__ u32 dec_tile_pr_body(const DecPrep& pr, u32 pos, u32 
     // A tile whose tokens all carry one byte v and that expands >= 20/7 = 2.86x its bytes (zero-
     // filled data: "v v 9" tokens) decodes to ttot copies of v: the partial chunk staged so far, filled, then rep4(v)
     // chunks, stored without the scatter and the fill; the new partial chunk is one key.
-    if (kFast && RLE_DEC_FAST && !st.head &&
+    if (kFast && !st.head &&
         7u * ttot >= 20u * (C - pos < kTileStep ? C - pos : kTileStep)) {   // (C > pos: the tile exists)
         const u32 v = (readlane(w[0], 0) >> (8u * st.d)) & 0xFFu;   // the tile's first token byte
         const u32 vv = rep4(v);
@@ -2158,14 +1929,11 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     RLE_STAMP(st.sp, 0);   // DMA wait + loop
     const u32x4 cur = *reinterpret_cast<const u32x4*>(cslot + 16u * lane);
     next();   // the slot is free once read
-    // RLE_DEC_UNIFORM_GATE (round 5): only after a single-value tile (st.sv), so that the test stays
-    // off the dependent chain of every other kind of tile (it cost configs[1] decode 0.56-0.7 us
-    // and the 64 KiB random / run-heavy kinds 2-3 %, profiles/r5b_ab.md, r5c_ab.md), while the long
+    // The uniform test only after a single-value tile (st.sv, round 5), so that it stays off the
+    // dependent chain of every other kind of tile (it cost configs[1] decode 0.56-0.7 us and the
+    // 64 KiB random / run-heavy kinds 2-3 %, profiles/r5b_ab.md, r5c_ab.md), while the long
     // zero-filled or single-byte stretches it is for take it from their second tile on.
-#ifndef RLE_DEC_UNIFORM_GATE
-#define RLE_DEC_UNIFORM_GATE 1
-#endif
-    if (kUni && RLE_DEC_UNIFORM && !(RLE_ABL & 32) && (st.sv || !RLE_DEC_UNIFORM_GATE) && !st.head &&
+    if (kUni && !(RLE_ABL & 32) && st.sv && !st.head &&
         pos + kSlot + 2u <= Co && st.out_pos + kUniformOut <= U) {
         u32 v;
         if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
@@ -2178,15 +1946,11 @@ __device__ __forceinline__ u32 dec_tile(const uint8_t* cslot, const Refill& next
     return dec_tile_pr<kFast, kChunks>(pr, pos, C, Co, U, lane, stage, dst, rso, st, kc, clut);
 }
 
-// ---------------------------------------------------------------- two literal tiles per step
-// The one-round decode kernel (configs[1]: every buffer's wave resident at once, 4-5 tiles of a
-// 4 KiB random buffer walked one after the other) is bound by each wave's chain of dependent tile
-// steps.  Two whole literal tiles (dec_tile_fast's conditions) are independent but for tile B's entry
-// phase (tile A's exit, a readlane of A's phase scan) and its output offset (A's total), so a step
-// takes both: both preparations, both literal analyses and both compactions, with nothing between
-// them that waits on the other, then A's store and B's.  dec_lit_an is dec_tile_fast<false>'s test
-// and offsets, branch-free (the pair decides once for both tiles); dec_lit_emit its compaction and
-// store.  Any other pair (a run, a tail tile, a general tile) is decoded one tile after the other.
+// ---------------------------------------------------------------- literal analysis, branch-free
+// dec_tile_fast<false>'s test and offsets without its stores (the decode in rounds, rle_round.h,
+// decides a tile's path before its output offset is known).  (Round 5 also walked two whole literal
+// tiles per step with it in the one-round kernel: a lone wave -2 %, configs[1] decode +6 %; not
+// kept)
 struct DecLit {
     u32 del, kept, oexcl, ttot;
     bool reject;
@@ -2223,107 +1987,6 @@ __device__ __forceinline__ DecLit dec_lit_an(const DecPrep& pr, u32 lane, u32 d)
     r.ttot = 16u * kOwnLanes - (u32)__builtin_popcountll(B1) - (u32)__builtin_popcountll(B2) + (u32)(B3 >> 63);
     return r;
 }
-// The tile's bytes with its deleted positions removed, stored at base + the lane's offset (the last
-// lane's bytes past the tile's output are rewritten by later stores of this wave).
-__device__ __forceinline__ void dec_lit_emit(const DecPrep& pr, const DecLit& f, u32 lane, const u32x4* clut, u32x4 rso,
-                                             u32 base, bool wt) {
-    const u32* w = pr.w;
-    const u32 dm = lane < kOwnLanes ? f.del : 0u;
-    const u32 t1 = (u32)__builtin_ctz(dm | 0x10000u);
-    const u32 t2 = (u32)__builtin_ctz((dm & (dm - 1u)) | 0x10000u);
-    u32 y[4] = {w[0], w[1], w[2], w[3]};
-    if (__builtin_amdgcn_ballot_w64(t2 < 16u)) {
-        const u32x4 s2 = clut[t2];
-        const u32 y3 = __builtin_amdgcn_perm(y[3], y[3], s2.w);
-        y[0] = __builtin_amdgcn_perm(y[1], y[0], s2.x);
-        y[1] = __builtin_amdgcn_perm(y[2], y[1], s2.y);
-        y[2] = __builtin_amdgcn_perm(y[3], y[2], s2.z);
-        y[3] = y3;
-    }
-    const u32x4 sel = clut[t1];
-    u32x4 o;
-    o.x = __builtin_amdgcn_perm(y[1], y[0], sel.x);
-    o.y = __builtin_amdgcn_perm(y[2], y[1], sel.y);
-    o.z = __builtin_amdgcn_perm(y[3], y[2], sel.z);
-    const u32 c3 = __builtin_amdgcn_perm(y[3], y[3], sel.w);
-    const u32 n0 = from_next_lane(o.x, 0u);
-    const u32 s3 = f.kept >= 16u ? 0x03020100u : f.kept == 15u ? 0x04020100u : 0x05040100u;
-    o.w = lane < kOwnLanes ? __builtin_amdgcn_perm(n0, c3, s3) : c3;
-    vstore(rso, f.kept ? base + f.oexcl : kOOB, o, wt);
-}
-#ifndef RLE_DEC_PAIR   // 1: the one-round decode kernel walks two tiles per step (dec_pair)
-#define RLE_DEC_PAIR 0   // r5r same process: configs[1] decode 9.39 -> 9.93 us with it (lone waves -2 %)
-#endif
-// Tiles at pos (slot A) and pos + 1008 (slot B).  Returns the store instructions issued after both
-// refills, or ~0u (the stream needs the exact serial path).
-template <u32 kChunks, bool kUni>
-__device__ __forceinline__ u32 dec_pair(const uint8_t* slotA, const uint8_t* slotB, const Refill& nxA, const Refill& nxB,
-                                        u32 pos, u32 C, u32 U, u32 lane, const DecEntry* tbl, uint8_t* stage, uint8_t* dst,
-                                        u32x4 rso, DecState& st, const DecK& kc, const u32x4* clut) {
-    constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
-    const u32x4 curA = *reinterpret_cast<const u32x4*>(slotA + 16u * lane);
-    const u32x4 curB = *reinterpret_cast<const u32x4*>(slotB + 16u * lane);
-    nxA();
-    nxB();
-    const u32 posB = pos + kTileStep;
-    const DecPrep prA = dec_prepare(curA, pos, C, C, lane, tbl, kc);
-    const DecPrep prB = dec_prepare(curB, posB, C, C, lane, tbl, kc);
-    if (RLE_DEC_FAST && !st.head && !prB.tail) {   // (prA.tail implies prB.tail)
-        const u32 NEa = (prA.xa >> 7) | (prA.xb << 1), NEb = (prB.xa >> 7) | (prB.xb << 1);
-        // cheap reject first (runs): at most 2 equal neighbours per owned lane, in both tiles
-        if (!(__builtin_amdgcn_ballot_w64(__builtin_popcount(~NEa & 0xFFFFu) > 2 ||
-                                          __builtin_popcount(~NEb & 0xFFFFu) > 2) & kOwned)) {
-            const u32 dA = st.d;
-            const u32 dB = bfe(readlane(prA.incl, kOwnLanes - 1u), 8u * dA, 8);
-            const DecLit a = dec_lit_an(prA, lane, dA);
-            const DecLit b = dec_lit_an(prB, lane, dB);
-            if (!__builtin_amdgcn_ballot_w64(a.reject || b.reject) && st.out_pos + a.ttot + b.ttot + 16u <= U) {
-                u32 rounds = 2u;
-                const u32 rel0 = st.out_pos - st.flushed;
-                if (rel0) {   // a general tile's partial chunk: store it (its bytes past rel0 are rewritten below)
-                    u32x4 x, y;
-                    dec_read_chunk(reinterpret_cast<const u32x4*>(stage + 32u), x, y);
-                    u32 L[8];
-                    dec_fill_scan(x, y, L);
-                    vstore(rso, lane == 0u ? st.flushed : kOOB, dec_fill_out(L, st.fillc), st.wt);
-                    wave_lds_sync();
-                    if (lane < 8u)
-                        *reinterpret_cast<__attribute__((address_space(3))) u32*>(sswz(lds_addr(stage) + 32u + 4u * lane)) = 0u;
-                    wave_lds_sync();
-                    ++rounds;
-                }
-                dec_lit_emit(prA, a, lane, clut, rso, st.out_pos, st.wt);
-                dec_lit_emit(prB, b, lane, clut, rso, st.out_pos + a.ttot, st.wt);
-                st.out_pos += a.ttot + b.ttot;
-                st.flushed = st.out_pos;
-                st.d = bfe(readlane(prB.incl, kOwnLanes - 1u), 8u * dB, 8);
-                st.prev = readlane(prB.w[3], kOwnLanes - 1u);
-                st.vrun = 0u;
-                st.sv = false;
-                return rounds;
-            }
-        }
-    }
-    // one after the other (dec_tile's uniform-tile test included)
-    auto one = [&](const u32x4 cur, const DecPrep& pr, u32 p) -> u32 {
-        if (kUni && RLE_DEC_UNIFORM && !(RLE_ABL & 32) && (st.sv || !RLE_DEC_UNIFORM_GATE) && !st.head &&
-            p + kSlot + 2u <= C && st.out_pos + kUniformOut <= U) {
-            u32 v;
-            if (dec_uniform_tile(cur, lane, kc.LM3, st.d, v)) {
-                const u32 r = dec_fill_run(v, kUniformOut, lane, stage, rso, st);
-                st.prev = readlane(cur.w, kOwnLanes - 1u);
-                return r;
-            }
-        }
-        return dec_tile_pr<true, kChunks>(pr, p, C, C, U, lane, stage, dst, rso, st, kc, clut);
-    };
-    const u32 r0 = one(curA, prA, pos);
-    if (r0 == ~0u) return ~0u;
-    const u32 r1 = one(curB, prB, posB);
-    if (r1 == ~0u) return ~0u;
-    return r0 + r1;
-}
-
 // After the last tile: outputs [flushed, end) = the partial chunk still staged (decoded positions
 // < out_pos), then zeros or the final unbounded token's byte (end = U for a stream's last segment,
 // end = out_pos for the others).  Bytes below flushed + head belong to the previous segment.

@@ -39,14 +39,12 @@
 #include "rle_fileops.h"
 #include "rle_mi355x.h"
 #include "rle_service.h"
+#include "rle_build.h"
 #include "rle_coop_limits.h"
 
 // Measured-slower host-path variants (call coalescing, pipelined staging) are compiled only into the
 // test library (build/librle_mi355x_testhooks.so) and `make variant` builds, never into the product
 // librle_mi355x.so (the measurements are in DESIGN.md §6).
-#ifndef RLE_VARIANTS
-#define RLE_VARIANTS 0
-#endif
 
 namespace {
 
@@ -184,9 +182,6 @@ size_t g_stage_cap = 32u << 20;
 // Test builds only (RLE_TEST_HOOKS=1: build/librle_mi355x_testhooks.so, never the product library):
 // RLE_MI355X_FAIL_ALLOC_ABOVE=<bytes> makes staging / device allocations larger than that fail as
 // if memory were exhausted, so the allocation-failure paths can be exercised.
-#ifndef RLE_TEST_HOOKS
-#define RLE_TEST_HOOKS 0
-#endif
 #if RLE_TEST_HOOKS
 size_t g_fail_above = SIZE_MAX;
 inline bool injected_failure(size_t n) { return n > g_fail_above; }

@@ -10,39 +10,17 @@
 
 namespace rle {
 
-#ifndef RLE_XCD_MAP
-#define RLE_XCD_MAP 1
-#endif
 constexpr u32 kXcds = 8;
 // Buffer of wave `wid` of workgroup `wg` when every XCD (workgroups are dealt to the 8 XCDs
 // round-robin) takes a contiguous slice of the batch instead of every 8th buffer: a batch whose
 // cost varies with a stride (e.g. i % 4) then still spreads evenly over the XCDs.
 __device__ __forceinline__ u32 xcd_buffer(u32 wg, u32 ngrid, u32 waves, u32 wid) {
-#if RLE_XCD_MAP
     const u32 per = ngrid / kXcds;   // launcher makes ngrid a multiple of 8
     return ((wg % kXcds) * per + wg / kXcds) * waves + wid;
-#else
-    (void)ngrid;
-    return wg * waves + wid;
-#endif
 }
 
-#ifndef RLE_NOWALK   // fixed-cost probe builds only (wrong output): no tiles walked
-#define RLE_NOWALK 0
-#endif
+#define RLE_NOWALK ((RLE_ABL & 128) != 0)   // fixed-cost probe builds only (wrong output): no tiles walked
 
-#ifndef RLE_DEC_PRIO   // decode wave priority by walk length (decode_kernel)
-#define RLE_DEC_PRIO 1
-#endif
-#ifndef RLE_STAGGER   // experiments: the waves sharing a SIMD start RLE_STAGGER * 64 cycles apart
-#define RLE_STAGGER 0
-#endif
-__device__ __forceinline__ void stagger() {
-#if RLE_STAGGER
-    const u32 slot = (u32)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) & 3u;   // HW_ID.WAVE_ID
-    for (u32 k = 0; k < slot; ++k) __builtin_amdgcn_s_sleep(RLE_STAGGER);
-#endif
-}
 
 // Diagnostic timeline builds (RLE_TIMELINE=1, never the product library): lane 0 of the wave of
 // buffer b < kTlWaves records s_memrealtime (100 MHz) at kernel entry [0], walk start [1], the start
@@ -87,8 +65,9 @@ constexpr u32 kEncWaves = RLE_ENC_WAVES;
 constexpr u32 kEncSmall = RLE_ENC_SMALL;
 constexpr u32 kEncBlock = kWave * kEncWaves;
 // kWtMode: the output store policy fixed at compile time (1 write-through, 2 write-back; 0 the launch
-// flag's bit 0 at run time), so that the tile steps carry no branch around each store
-// (RLE_WT_STATIC, round 5)
+// flag's bit 0 at run time), so that the tile steps carry no branch around each store (round 5).
+// Two tile slots per wave (kDepth, the instantiation names of the profiles; deeper rings measured no
+// faster).
 template <u32 kDepth = 2u, u32 kWtMode = 0u>
 __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
@@ -98,7 +77,8 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
                                                            uint64_t* __restrict__ out_len,
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt) {
     const unsigned long long tl0 = tl_now();
-    constexpr u32 kSlotsB = kDepth > 2u ? kDepth * kSlot : 2u * kEncSlot;   // (ring slots: 1008-byte tiles)
+    static_assert(kDepth == 2u, "two tile slots per wave");
+    constexpr u32 kSlotsB = 2u * kEncSlot;
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kEncWaves * kSlotsB];
     __shared__ __attribute__((aligned(16))) uint8_t stage_all[kEncWaves * kEncStage];
     __shared__ __attribute__((aligned(16))) u32 elut_all[kEncWaves * kInsWaveWords];
@@ -139,38 +119,26 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
     for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
     st.sp.last = memtime();
 #endif
-    stagger();
     tl_mark(b, 1, lane);
     // 1024-byte tiles where they save a tile, up to kEncSmall (rle_device.h, enc_tile<true>)
     if (enc_ntiles_for(U) < ntiles_for(U) && U <= kEncSmall) {
-        if (RLE_ENC_PAIR)   // two tiles per step (rle_device.h enc_pair)
-            walk_pairs<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
-                       [&](u32 t, const uint8_t* sa, const uint8_t* sb, const Refill& na, const Refill& nb) {
-                           tl_mark(b, 2u + t, lane);
-                           tl_mark(b, 3u + t, lane);
-                           return enc_pair<true>(sa, sb, na, nb, t * kEncStep, U, lane, stage, dst, rso, st, kc, elut);
-                       },
-                       [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                           tl_mark(b, 2u + t, lane);
-                           return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
-                       });
-        else
-            walk_tiles<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
-                                       [&](u32 t, const uint8_t* cs, const Refill& nx) {
-                                           tl_mark(b, 2u + t, lane);
-                                           return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
-                                       });
+        // two tiles per step (rle_device.h enc_pair)
+        walk_pairs<kEncStep, true>(rsi, 0u, RLE_NOWALK ? 0u : enc_ntiles_for(U), lane, slots,
+                   [&](u32 t, const uint8_t* sa, const uint8_t* sb, const Refill& na, const Refill& nb) {
+                       tl_mark(b, 2u + t, lane);
+                       tl_mark(b, 3u + t, lane);
+                       return enc_pair<true>(sa, sb, na, nb, t * kEncStep, U, lane, stage, dst, rso, st, kc, elut);
+                   },
+                   [&](u32 t, const uint8_t* cs, const Refill& nx) {
+                       tl_mark(b, 2u + t, lane);
+                       return enc_tile<true, true>(cs, nx, t * kEncStep, U, U, lane, stage, dst, rso, st, kc, elut);
+                   });
     } else {
         auto tile = [&](u32 t, const uint8_t* cs, const Refill& nx) {
             tl_mark(b, 2u + t, lane);
             return enc_tile<false, true>(cs, nx, t * kTileStep, U, U, lane, stage, dst, rso, st, kc, elut);
         };
-        if constexpr (kDepth > 2u) {
-            walk_ring_prime<kDepth>(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots);
-            walk_ring<kDepth>(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, tile);
-        } else {
-            walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, tile);
-        }
+        walk_tiles(rsi, 0u, RLE_NOWALK ? 0u : ntiles_for(U), lane, slots, tile);
     }
     RLE_STAMP(st.sp, 6);   // drain
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past C
@@ -198,11 +166,22 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const uint8_t* __rest
 constexpr u32 kDecWaves = RLE_DEC_WAVES;
 constexpr u32 kDecBlock = kWave * kDecWaves;
 // Issue order of a large decode batch (longest first): buffer indices sorted by descending tile
-// count, a counting sort over kOrderBuckets clamped keys (order inside a bucket is arbitrary).
-// Heavy buffers then start in the first residency round, and the four waves of a workgroup,
-// which hold its LDS until the last one ends, get buffers of similar cost.  Outputs do not depend
-// on the order.  Two small launches, histogram and scatter, over hist[] and cursor[] (both zeroed
-// by the launcher).
+// count, a counting sort over kOrderBuckets clamped keys.  Heavy buffers then start in the first
+// residency round, and the four waves of a workgroup, which hold its LDS until the last one ends,
+// get buffers of similar cost.  Outputs do not depend on the order.
+//
+// One launch, no global counts (round 5): each workgroup sorts its own kLocalChunk buffers longest
+// first (its LDS histogram, a descending scan of it, each buffer's place = its bucket's start + its
+// rank in the bucket) into order[chunk * kLocalChunk ...], and the decode kernel interleaves the
+// F = n / kLocalChunk full chunks (slot s takes place s / F of chunk s % F; the last partial chunk
+// follows them): the i-th heaviest buffers of every chunk are issued together, which on batches
+// whose chunks hold similar mixes (every bench and server batch) is the global longest-first order.
+// Ties inside a bucket fall in LDS-atomic order, which scatters the concurrently issued buffers'
+// offsets.  Measured and not kept: a global histogram + scatter in two launches
+// (r5t: -1.8 % on dec64k without them), ties in index order or groups of consecutive places
+// (+4-8 %: same-rank buffers of every chunk at a 16 MiB stride pile onto the same channels), ranks
+// permuted per chunk, larger chunks (512-2048 buffers), each XCD walking its own slice, the
+// metadata copied into issue order (all within +-1 % or slower).
 constexpr u32 kOrderBuckets = 2048;
 __device__ __forceinline__ u32 order_key(uint64_t C) {
     const uint64_t t = (C + kTileStep - 1u) / kTileStep;
@@ -227,20 +206,11 @@ __device__ __forceinline__ u32 grouped_add(u32* hist, u32 key, bool on, u32 lane
     }
     return pos;
 }
-// Each workgroup takes kOrderChunk consecutive buffers (kOrderPer per thread), counts them in an
-// LDS histogram and adds its non-empty buckets to the global one: one global atomic per bucket and
-// workgroup.
-constexpr u32 kOrderPer = 4;
-constexpr u32 kOrderChunk = 256u * kOrderPer;
-#ifndef RLE_ORDER_SPREAD   // 1: ranks inside a bucket permuted per chunk (dec_order_local_kernel)
-#define RLE_ORDER_SPREAD 0
-#endif
-#ifndef RLE_ORDER_STABLE   // 1: ties inside a chunk keep index order (the waves rank one after another)
-#define RLE_ORDER_STABLE 0
-#endif
-template <u32 kPer = kOrderPer, bool kStable = false>   // buffers per thread (a workgroup's chunk: 256 kPer buffers)
-__device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kPer],
-                                            u32 (&rank)[kPer]) {
+constexpr u32 kLocalPer = 1u, kLocalChunk = 256u * kLocalPer;   // buffers per thread / per workgroup
+// The chunk's keys, its LDS histogram and each buffer's rank in its bucket.
+__device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, u32* lh, u32 (&key)[kLocalPer],
+                                            u32 (&rank)[kLocalPer]) {
+    constexpr u32 kPer = kLocalPer;
     const u32 t = threadIdx.x, lane = t & (kWave - 1);
     // the lengths' loads first, so their latency overlaps the histogram's zeroing and barrier
     const u32 i0 = blockIdx.x * (256u * kPer) + t;
@@ -251,103 +221,18 @@ __device__ __forceinline__ void order_local(const uint64_t* in_len, uint32_t n, 
     __syncthreads();
 #pragma unroll
     for (u32 j = 0; j < kPer; ++j) key[j] = i0 + 256u * j < n ? order_key(len[j]) : 0u;
-    if (kStable && kPer == 1u) {   // wave w ranks after waves 0..w-1: equal keys in index order
-        const u32 wv = threadIdx.x / kWave;
-        for (u32 w = 0; w < 256u / kWave; ++w) {
-            if (wv == w) rank[0] = grouped_add(lh, key[0], i0 < n, lane);
-            __syncthreads();
-        }
-        return;
-    }
 #pragma unroll
     for (u32 j = 0; j < kPer; ++j) rank[j] = grouped_add(lh, key[j], i0 + 256u * j < n, lane);
     __syncthreads();
 }
-__global__ __launch_bounds__(256) void dec_order_hist_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
-                                                             uint32_t* __restrict__ hist) {
-    __shared__ u32 lh[kOrderBuckets];
-    u32 key[kOrderPer], rank[kOrderPer];
-    order_local(in_len, n, lh, key, rank);
-    for (u32 k = threadIdx.x; k < kOrderBuckets; k += 256u)
-        if (lh[k]) atomicAdd(&hist[k], lh[k]);
-}
-// The same local counts again.  Every workgroup scans the global counts into descending bucket
-// starts (thread t: the 8 buckets from B-1-8t down), each non-empty bucket of the workgroup takes
-// its range inside the bucket with one atomic on cursor[], and each buffer's place is bucket
-// start + range base + its rank inside the workgroup.
-__global__ __launch_bounds__(256) void dec_order_scatter_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
-                                                                const uint32_t* __restrict__ hist,
-                                                                uint32_t* __restrict__ cursor,
-                                                                uint32_t* __restrict__ order) {
-    __shared__ u32 lh[kOrderBuckets];
-    __shared__ u32 start[kOrderBuckets];
-    __shared__ u32 wsum[4];
-    constexpr u32 kPerT = kOrderBuckets / 256u;
-    const u32 t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
-    u32 c[kPerT], sum = 0u;
-#pragma unroll
-    for (u32 j = 0; j < kPerT; ++j) {
-        c[j] = hist[kOrderBuckets - 1u - (kPerT * t + j)];
-        sum += c[j];
-    }
-    const u32 incl = wave_scan_incl(sum, 0u, OpAdd());
-    if (lane == kWave - 1) wsum[wv] = incl;
-    u32 key[kOrderPer], rank[kOrderPer];
-    order_local(in_len, n, lh, key, rank);   // (its barriers also publish wsum)
-    u32 base = incl - sum;
-    for (u32 w = 0; w < wv; ++w) base += wsum[w];
-#pragma unroll
-    for (u32 j = 0; j < kPerT; ++j) {
-        start[kOrderBuckets - 1u - (kPerT * t + j)] = base;
-        base += c[j];
-    }
-    for (u32 k = t; k < kOrderBuckets; k += 256u)
-        if (lh[k]) lh[k] = atomicAdd(&cursor[k], lh[k]);
-    __syncthreads();
-    const u32 i0 = blockIdx.x * kOrderChunk + threadIdx.x;
-#pragma unroll
-    for (u32 j = 0; j < kOrderPer; ++j) {
-        const u32 i = i0 + 256u * j;
-        if (i < n) order[start[key[j]] + lh[key[j]] + rank[j]] = i;
-    }
-}
-
-// Issue order in one launch and without global counts (RLE_ORDER_LOCAL, round 5): each workgroup sorts
-// its own kLocalChunk buffers longest first (its LDS histogram, a descending scan of it, each buffer's
-// place = its bucket's start + its rank in the bucket) into order[chunk * kLocalChunk ...], and the
-// decode kernel interleaves the F = n / kLocalChunk full chunks (slot s takes place s / F of chunk
-// s % F; the last partial chunk follows them): the i-th heaviest buffers of every chunk are issued
-// together, which on batches whose chunks hold similar mixes (every bench and server batch) is the
-// global longest-first order without the memset, the second launch and the global atomics.
-#ifndef RLE_ORDER_LOCAL_PER   // buffers per thread of the chunk-local sort (chunks of 256 x this)
-#define RLE_ORDER_LOCAL_PER 1
-#endif
-constexpr u32 kLocalPer = RLE_ORDER_LOCAL_PER, kLocalChunk = 256u * kLocalPer;
-#ifndef RLE_ORDER_DESC   // 1: the order holds each buffer's metadata in issue order (OrderDesc)
-#define RLE_ORDER_DESC 0
-#endif
-// RLE_ORDER_DESC: order[] entries are the buffers' metadata copied into issue order, so a decode
-// wave makes one dependent round trip for its buffer (its slot's descriptor) instead of two (its
-// slot's index, then the five metadata words at that index).
-struct OrderDesc {
-    uint64_t in_off, in_len, out_off, out_len, cap;
-    uint32_t b, pad;
-};
-static_assert(sizeof(OrderDesc) == 48u, "OrderDesc: three 16-byte stores");
-struct OrderMeta {   // the metadata arrays RLE_ORDER_DESC copies (cap: NULL = out_len)
-    const uint64_t* in_off;
-    const uint64_t* out_off;
-    const uint64_t* out_len;
-    const uint64_t* cap;
-};
 __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
-                                                              uint32_t* __restrict__ order, OrderMeta meta) {
+                                                              uint32_t* __restrict__ order) {
     __shared__ u32 lh[kOrderBuckets];
     __shared__ u32 wsum[4];
     constexpr u32 kPerT = kOrderBuckets / 256u;
     const u32 t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
     u32 key[kLocalPer], rank[kLocalPer];
-    order_local<kLocalPer, RLE_ORDER_STABLE != 0>(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
+    order_local(in_len, n, lh, key, rank);   // (ends with a barrier: lh holds the chunk's counts)
     // thread t: the 8 buckets from B-1-8t down, in descending bucket order
     u32 c[kPerT], sum = 0u;
 #pragma unroll
@@ -371,96 +256,26 @@ __global__ __launch_bounds__(256) void dec_order_local_kernel(const uint64_t* __
     for (u32 j = 0; j < kLocalPer; ++j) {
         const u32 i = i0 + 256u * j;
         if (i >= n) continue;
-        u32 r = rank[j];
-        if (RLE_ORDER_SPREAD) {
-            // a permutation inside the bucket (equal keys: longest first is kept) that differs from
-            // chunk to chunk: the chunks' same-rank slots, issued together, take different offsets
-            // inside their chunks, not buffers at a 16 MiB stride (r5at)
-            const u32 nvalid = n - blockIdx.x * kLocalChunk < kLocalChunk ? n - blockIdx.x * kLocalChunk : kLocalChunk;
-            const u32 m = (key[j] > 0u ? lh[key[j] - 1u] : nvalid) - lh[key[j]];
-            r = (r * 263u + blockIdx.x * 97u) % m;
-        }
-        const u32 place = blockIdx.x * kLocalChunk + lh[key[j]] + r;
-        if (RLE_ORDER_DESC) {
-            OrderDesc d;
-            d.in_off = meta.in_off[i];
-            d.in_len = in_len[i];
-            d.out_off = meta.out_off[i];
-            d.out_len = meta.out_len[i];
-            d.cap = (meta.cap ? meta.cap : meta.out_len)[i];
-            d.b = i;
-            d.pad = 0u;
-            reinterpret_cast<OrderDesc*>(order)[place] = d;
-        } else {
-            order[place] = i;
-        }
+        order[blockIdx.x * kLocalChunk + lh[key[j]] + rank[j]] = i;
     }
 }
-#ifndef RLE_ORDER_LOCAL
-#define RLE_ORDER_LOCAL 1
-#endif
 // The buffer a decode wave takes at issue slot s of an order made by dec_order_local_kernel.
-#ifndef RLE_ORDER_GROUP   // consecutive slots that take consecutive places of one chunk (1, 2, 4, ... 256)
-#define RLE_ORDER_GROUP 1
-#endif
 __device__ __forceinline__ u32 order_slot_local(u32 s, u32 n) {
     const u32 F = n / kLocalChunk;   // full chunks, interleaved; the partial one after them
     if (s >= F * kLocalChunk) return s;
-    constexpr u32 G = RLE_ORDER_GROUP;
-    static_assert(kLocalChunk % G == 0u, "RLE_ORDER_GROUP divides the chunk");
-    const u32 q = s / G;   // groups of G slots: group q takes places (q / F) G .. + G - 1 of chunk q % F
-    return (q % F) * kLocalChunk + (q / F) * G + s % G;
-}
-#ifndef RLE_ORDER_XCD   // 1: each XCD interleaves only the chunks of its own contiguous slice
-#define RLE_ORDER_XCD 0
-#endif
-// The place in order[] that workgroup wg's wave wid takes (n: none) with RLE_ORDER_XCD: XCD x =
-// wg % 8 owns places [x R, x R + L) (R = its slots, L clipped at n), as xcd_buffer gives it buffers;
-// its k-th slot takes place k / F of its k % F-th full chunk (F of them inside the slice), then the
-// slice's head and tail fragments in index order.  Each XCD walks its own slice longest first, so
-// the waves in flight on one XCD stay within an eighth of the batch instead of all of it.
-__device__ __forceinline__ u32 order_place_xcd(u32 wg, u32 ngrid, u32 wid, u32 n) {
-    const u32 R = ngrid / kXcds * kDecWaves;   // launcher makes ngrid a multiple of 8
-    const u32 a = (wg % kXcds) * R;
-    const u32 k = (wg / kXcds) * kDecWaves + wid;
-    if (a >= n || k >= n - a) return n;
-    const u32 L = n - a < R ? n - a : R;
-    const u32 c0 = (a + kLocalChunk - 1u) / kLocalChunk, c1 = (a + L) / kLocalChunk;
-    const u32 F = c1 > c0 ? c1 - c0 : 0u;
-    if (k < F * kLocalChunk) return (c0 + k % F) * kLocalChunk + k / F;
-    if (F == 0u) return a + k;
-    const u32 r = k - F * kLocalChunk, h = c0 * kLocalChunk - a;
-    return r < h ? a + r : c1 * kLocalChunk + (r - h);
+    return (s % F) * kLocalChunk + s / F;   // slot s takes place s / F of chunk s % F
 }
 
 // kChunks: staging chunks per wave (32 B each).  192 hold any tile's output in one pass; the
 // launcher takes 96 (3 KiB per wave: 7 workgroups per CU instead of 4) for batches past one
 // residency round, where the extra waves hide more latency than the two-pass staging of the
 // output-heavy tiles costs.
-#ifndef RLE_DEC_DEPTH_LARGE   // tile slots per wave of the large-batch decode (walk_ring; 2: walk_tiles)
-#define RLE_DEC_DEPTH_LARGE 2     // r5c same process: 3 / 4 slots +4-6 % on 64 KiB runs50 / runs90, dec64k +1.2 / +1.7 %
-#endif
-// The uniform-tile test (dec_uniform_tile) per kernel.  r5b / r5c same process (profiles/r5b_ab.md,
-// r5c_ab.md): in the one-round kernel (configs[1]) it cost decode 0.56-0.7 us (10.03 -> 9.47 us),
-// so it is off there; in the large-batch kernel it still pays on the dec64k mix (420.9 against
-// 423.5 us without), although the single-kind 64 KiB batches other than zero are 2-3 % faster
-// without it.
-#ifndef RLE_DEC_UNIFORM_ONE
-#define RLE_DEC_UNIFORM_ONE 1   // (gated by RLE_DEC_UNIFORM_GATE: tried only after a single-value tile)
-#endif
-#ifndef RLE_DEC_UNIFORM_LARGE
-#define RLE_DEC_UNIFORM_LARGE 1
-#endif
-// kDepth: tile slots per wave (walk_ring past 2).  Few-buffer launches (kFewBuffers, the drop-in's
-// single calls) may take kFewDepth slots (RLE_FEW_DEPTH > 2): one wave walking a file over PCIe
-// (zero-copy) or from HBM with more loads in flight.  Measured (r5e, profiles/r5e_call_latency.md):
-// 8 slots were no faster than 2 at any size from 4 KiB to 128 KiB (random 24 KiB: 36.5 / 36.5 us
-// against 32.3 / 31.9 us per compress / decompress call): a lone wave's walk is bound by its tiles'
-// dependent chains, not by loads in flight.  Off (2).
-#ifndef RLE_FEW_DEPTH
-#define RLE_FEW_DEPTH 2
-#endif
-constexpr u32 kFewDepth = RLE_FEW_DEPTH;
+// Two tile slots per wave (walk_tiles).  Measured and not kept: 3 / 4 slots in the
+// large-batch kernel (r5c: 64 KiB runs50 / runs90 +4-6 %, dec64k +1.2 / +1.7 %), 8 slots for the
+// drop-in's single calls (r5e: no faster from 4 KiB to 128 KiB: a lone wave's walk is bound by its
+// tiles' dependent chains, not by loads in flight).  The uniform-tile test (dec_uniform_tile, gated:
+// tried only after a single-value tile) runs in both kernels.  (kDepthT: kept 0, the instantiation
+// names of the profiles.)
 template <u32 kChunks, u32 kDepthT = 0u, u32 kWtMode = 0u>   // (kWtMode: as encode_kernel's)
 __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ in_off,
@@ -472,7 +287,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
                                                            uint32_t* __restrict__ status, uint32_t n, uint32_t wt,
                                                            const uint32_t* __restrict__ order) {
     const unsigned long long tl0 = tl_now();
-    constexpr u32 kDepth = kDepthT ? kDepthT : (kChunks >= 191u ? 2u : (u32)RLE_DEC_DEPTH_LARGE);
+    static_assert(kDepthT == 0u, "two tile slots per wave");
+    constexpr u32 kDepth = 2u;
     __shared__ __attribute__((aligned(16))) uint8_t slots_all[kDecWaves * kDepth * kSlot];
     constexpr u32 kStageB = 32u * kChunks;
     __shared__ __attribute__((aligned(128))) uint8_t stage_all[kDecWaves * kStageB];
@@ -486,49 +302,20 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     const u32 wid = uniform(threadIdx.x / kWave);
     // with an issue order, workgroups take its ranks in dispatch order (the heavy buffers first,
     // spread over every XCD); else each XCD takes a contiguous slice of the batch
+    // (Measured and not kept, DESIGN.md §4: heavy / light workgroup blocks or waves alternating, the
+    // order ignored, each XCD walking its own slice, the metadata copied into issue order.)
     u32 b;
-#ifndef RLE_ORDER_MODE   // A/B only: 1 heavy / light workgroup blocks of 8 alternate; 2 heavy / light waves
-#define RLE_ORDER_MODE 0     // alternate inside a workgroup; 3 the order ignored (index order)
-#endif
-    if (order && RLE_ORDER_MODE != 3) {
+    if (order) {
         u32 slot = blockIdx.x * kDecWaves + wid;
-        if (RLE_ORDER_XCD && RLE_ORDER_LOCAL && RLE_ORDER_MODE == 0) {
-            slot = uniform(order_place_xcd(blockIdx.x, gridDim.x, wid, n));
-        } else if (RLE_ORDER_MODE == 1 && (gridDim.x & 7u) == 0u) {
-            const u32 nb = gridDim.x >> 3, h = blockIdx.x >> 3;
-            const u32 ph = (h & 1u) ? nb - 1u - (h >> 1) : (h >> 1);
-            slot = (8u * ph + (blockIdx.x & 7u)) * kDecWaves + wid;
-        } else if (RLE_ORDER_MODE == 2 && slot < n) {
-            slot = (slot & 1u) ? n - 1u - (slot >> 1) : (slot >> 1);
-        }
-        if (!(RLE_ORDER_XCD && RLE_ORDER_MODE == 0) && RLE_ORDER_LOCAL && slot < n) slot = uniform(order_slot_local(slot, n));
-        if (RLE_ORDER_DESC && RLE_ORDER_LOCAL) {
-            b = slot;   // (the descriptor's index below)
-        } else {
-            b = slot < n ? uniform(order[slot]) : n;
-        }
+        if (slot < n) slot = uniform(order_slot_local(slot, n));
+        b = slot < n ? uniform(order[slot]) : n;
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
     }
     // all five per-buffer words are loaded at once, unconditionally (index clamped; n >= 1)
-    uint64_t C64, U64, cap, ioff, ooff;
-    if (RLE_ORDER_DESC && RLE_ORDER_LOCAL && order && RLE_ORDER_MODE != 3) {
-        const OrderDesc* od = reinterpret_cast<const OrderDesc*>(order) + (b < n ? b : 0u);
-        C64 = od->in_len;
-        U64 = od->out_len;
-        cap = od->cap;
-        ioff = od->in_off;
-        ooff = od->out_off;
-        b = b < n ? uniform(od->b) : n;
-    } else {
-        const u32 bi = b < n ? b : 0u;
-        const uint64_t* capp = out_cap ? out_cap : out_len;
-        C64 = in_len[bi];
-        U64 = out_len[bi];
-        cap = capp[bi];
-        ioff = in_off[bi];
-        ooff = out_off[bi];
-    }
+    const u32 bi = b < n ? b : 0u;
+    const uint64_t* capp = out_cap ? out_cap : out_len;
+    const uint64_t C64 = in_len[bi], U64 = out_len[bi], cap = capp[bi], ioff = in_off[bi], ooff = out_off[bi];
     tl_mark(b, 0, lane);
     tl_put(b, 13, tl0, lane);
     tl_ids(b, lane);
@@ -545,8 +332,8 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     tl_mark(b, 14u + 0u * ntiles, lane);   // (diagnostic builds: the metadata has arrived)
     // Issue priority by walk length (log2 buckets of the tile count): where a SIMD holds waves of
     // unequal walks, the longest are the launch's critical path, and the short ones fill their
-    // stalls.  RLE_DEC_PRIO: 0 off, 1 the one-round kernel (kChunks >= 191) only, 2 every size.
-    if (RLE_DEC_PRIO == 2 || (RLE_DEC_PRIO == 1 && kChunks >= 191u)) {
+    // stalls: the one-round kernel (kChunks >= 191) only (every size measured within +-1 %, r5ah).
+    if (kChunks >= 191u) {
         if (ntiles >= 32u) __builtin_amdgcn_s_setprio(3);
         else if (ntiles >= 8u) __builtin_amdgcn_s_setprio(2);
         else if (ntiles >= 3u) __builtin_amdgcn_s_setprio(1);
@@ -559,9 +346,7 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
     // barrier publishes them, normally before the first tile's data has landed.  (At kernel start
     // every wave's loads queue at once: one copy per workgroup instead of per wave keeps the
     // table traffic off the first tiles' path.)
-    stagger();
-    if constexpr (kDepth == 2u) walk_prime(rsi, 0u, ntiles, lane, slots);
-    else walk_ring_prime<kDepth>(rsi, 0u, ntiles, lane, slots);
+    walk_prime(rsi, 0u, ntiles, lane, slots);
     tl_mark(b, 15, lane);   // (diagnostic builds: the first tiles' loads issued)
     if (wid == 0u) {
         const u32x4 rt = make_rsrc(&kDecTable, (u32)sizeof(DecTable));
@@ -585,7 +370,6 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         }
         const u32x4 rso = make_rsrc(dst, U);
         DecState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, kWtMode ? kWtMode == 1u : (wt & kLaunchWt) != 0u, {}};
-        st.hold_ok = true;
         const DecK kc = dec_k();
 #if RLE_STAMPS
         for (u32 k = 0; k < kStampSegs; ++k) st.sp.acc[k] = 0;
@@ -594,25 +378,13 @@ __global__ __launch_bounds__(kDecBlock) void decode_kernel(const uint8_t* __rest
         tl_mark(b, 1, lane);
         auto tile = [&](u32 t, const uint8_t* cs, const Refill& nx) {
             tl_mark(b, 2u + t, lane);
-            return dec_tile<true, kChunks, (kChunks >= 191u ? RLE_DEC_UNIFORM_ONE : RLE_DEC_UNIFORM_LARGE) != 0>(
-                cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
+            return dec_tile<true, kChunks, true>(cs, nx, t * kTileStep, C, C, U, lane, tbl, stage, dst, rso, st, kc, clut);
         };
-        bool serial;
-        constexpr bool kUniK = (kChunks >= 191u ? RLE_DEC_UNIFORM_ONE : RLE_DEC_UNIFORM_LARGE) != 0;
-        if constexpr (kDepth == 2u && kChunks >= 191u && RLE_DEC_PAIR)   // one round: two tiles per step
-            serial = walk_pairs(rsi, 0u, ntiles, lane, slots,
-                                [&](u32 t, const uint8_t* sa, const uint8_t* sb, const Refill& na, const Refill& nb) {
-                                    return dec_pair<kChunks, kUniK>(sa, sb, na, nb, t * kTileStep, C, U, lane, tbl, stage,
-                                                                    dst, rso, st, kc, clut);
-                                },
-                                tile, true);
-        else if constexpr (kDepth == 2u) serial = walk_tiles(rsi, 0u, ntiles, lane, slots, tile, true);
-        else serial = walk_ring<kDepth>(rsi, 0u, ntiles, lane, slots, tile);
+        const bool serial = walk_tiles(rsi, 0u, ntiles, lane, slots, tile, true);
         RLE_STAMP(st.sp, 7);   // drain after the last tile
         u32 stat = RLE_STATUS_OK;
         if (serial) stat = dec_serial(src, C, U, cap, dst, lane, stage, kStageB);
         else {
-            dec_release(lane, rso, st);
             dec_finish(st, U, lane, stage, rso, dst);
             stat = dec_tiled_status(st, U);
         }
@@ -679,13 +451,9 @@ __global__ void gen_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict
 // work.  Each wave streams its buffer's C bytes in through decode_kernel's tile walk (1 KiB LDS-DMA
 // tiles, two in flight, walk_tiles) and writes its U bytes out in 16-byte-per-lane stores, each tile
 // taking its share of the output; workgroups, LDS (7 per CU) and the issue order as decode_kernel<96>.
-// Not the codec: the output bytes are the tiles' bytes repeated.
-#ifndef RLE_PATTERN_SHIFT   // experiments: stores line-aligned by shifting lanes (tile shares unchanged)
-#define RLE_PATTERN_SHIFT 0
-#endif
-#ifndef RLE_PATTERN_ALIGN   // experiments: each tile's output share ends on a multiple of this (16: the decode's stores)
-#define RLE_PATTERN_ALIGN 16
-#endif
+// Not the codec: the output bytes are the tiles' bytes repeated.  Each tile's share ends on a
+// 16-byte chunk, as the decode's stores do (128-byte shares measured 3 % faster, lanes shifted onto
+// lines 0.6-1.1 %: r5ap / r5aq).
 constexpr u32 kPatternPad = kDecWaves * 32u * 96u + (u32)sizeof(DecTable) + kCompactEntries * 16u;
 __global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __restrict__ in,
                                                             const uint64_t* __restrict__ in_off,
@@ -702,29 +470,15 @@ __global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __res
     u32 b;
     if (order) {
         const u32 slot = blockIdx.x * kDecWaves + wid;
-        const u32 place = RLE_ORDER_XCD ? order_place_xcd(blockIdx.x, gridDim.x, wid, n)
-                                        : slot < n ? order_slot_local(slot, n) : n;
-        b = place;
-        if (!RLE_ORDER_DESC) b = place < n ? uniform(order[uniform(place)]) : n;
+        const u32 place = slot < n ? order_slot_local(slot, n) : n;
+        b = place < n ? uniform(order[uniform(place)]) : n;
     } else {
         b = xcd_buffer(blockIdx.x, gridDim.x, kDecWaves, wid);
     }
     b = uniform(b);
     if (b >= n) return;
     auto u64 = [](uint64_t x) { return (uint64_t)uniform((u32)x) | ((uint64_t)uniform((u32)(x >> 32)) << 32); };
-    uint64_t C64, U64, ioff, ooff;
-    if (RLE_ORDER_DESC && order) {   // the decode's one round trip (its slot's descriptor)
-        const OrderDesc* od = reinterpret_cast<const OrderDesc*>(order) + b;
-        C64 = u64(od->in_len);
-        U64 = u64(od->out_len);
-        ioff = u64(od->in_off);
-        ooff = u64(od->out_off);
-    } else {
-        C64 = u64(in_len[b]);
-        U64 = u64(out_len[b]);
-        ioff = u64(in_off[b]);
-        ooff = u64(out_off[b]);
-    }
+    const uint64_t C64 = u64(in_len[b]), U64 = u64(out_len[b]), ioff = u64(in_off[b]), ooff = u64(out_off[b]);
     if (C64 > kMaxBufferBytes || U64 > kMaxBufferBytes) return;
     const u32 C = (u32)C64, U = (u32)U64;
     const uint8_t* src = in + ioff;
@@ -738,13 +492,11 @@ __global__ __launch_bounds__(kDecBlock) void pattern_kernel(const uint8_t* __res
     walk_tiles(rsi, 0u, ntiles, lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
         nx();
-        const u32 upto = t + 1u == ntiles ? U : (u32)(((uint64_t)(t + 1u) * U / ntiles) & ~(uint64_t)(RLE_PATTERN_ALIGN - 1));
+        const u32 upto = t + 1u == ntiles ? U : (u32)(((uint64_t)(t + 1u) * U / ntiles) & ~(uint64_t)15u);
         u32 k = 0;
-        // RLE_PATTERN_SHIFT: the stores start on the 128-byte line before `written` (lanes before it idle)
-        const u32 r = RLE_PATTERN_SHIFT ? ((rso.x >> 4) + (written >> 4)) & 7u : 0u;
-        const u32 nst = upto > written ? (upto - written + 16u * r + 16u * kWave - 1u) / (16u * kWave) : 0u;
+        const u32 nst = upto > written ? (upto - written + 16u * kWave - 1u) / (16u * kWave) : 0u;
         for (; k < nst; ++k) {
-            const u32 a = written - 16u * r + 16u * (k * kWave + lane);   // (wraps below 0: never stored)
+            const u32 a = written + 16u * (k * kWave + lane);
             vstore(rso, a >= written && a < upto ? a : kOOB, v, false);
         }
         written = upto;
@@ -849,14 +601,10 @@ uint32_t store_policy(uint32_t n, bool enc) {
 // Decode batches past one residency round of the chip (4 workgroups of 4 waves per CU) are
 // issued longest first; RLE_MI355X_DEC_ORDER=0 turns that off.
 constexpr uint32_t kDecRound = 4096;
-constexpr uint32_t kFewBuffers = 16;   // launches of up to this many buffers take the deep tile ring
 #ifndef RLE_DEC_CHUNKS_LARGE   // staging chunks of the decode kernel for batches past kDecRound
 #define RLE_DEC_CHUNKS_LARGE 96
 #endif
 constexpr uint32_t kDecChunksLarge = RLE_DEC_CHUNKS_LARGE;
-#ifndef RLE_WT_STATIC   // 1: the codec kernels instantiated per store policy (no run-time branch per store)
-#define RLE_WT_STATIC 1
-#endif
 // The large-batch decode in rounds (rle_round.h): waves per workgroup (4, 8 or 16; 0 off), for
 // batches past one residency round whose largest stream is at least kRoundMinIn bytes (the sized
 // entry points know it).  RLE_MI355X_DEC_ROUND overrides; tests switch it with rle_mi355x_set_dec_round.
@@ -870,9 +618,6 @@ bool dec_order_enabled() {
     return on;
 }
 
-#ifndef RLE_ORDER_CACHE   // 1: per-(device, stream) cached issue-order arrays
-#define RLE_ORDER_CACHE 1
-#endif
 // The issue order's device array.  A hipFreeAsync + hipMallocAsync pair per launch left a 5.8 us gap
 // on the queue between back-to-back large decodes (profiles/r5an_order_gap.md); instead each
 // (device, stream handle) keeps a grow-only array in one of kOrderStreams slots (launches being
@@ -924,7 +669,7 @@ void order_acquire(OrderArray& o, hipStream_t s, size_t bytes) {
     o.s = s;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
     int dev = -1;
-    if (RLE_ORDER_CACHE && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
         hipGetDevice(&dev) == hipSuccess) {
         o.lk = std::unique_lock<std::mutex>(g_order_mu);
         OrderSlot* e = nullptr;
@@ -1012,9 +757,7 @@ int encode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
     const uint32_t pol = store_policy(n, true);
-    auto kern = !RLE_WT_STATIC ? rle::encode_kernel<2u> : pol ? rle::encode_kernel<2u, 1u> : rle::encode_kernel<2u, 2u>;
-    if constexpr (rle::kFewDepth > 2u)
-        if (n <= kFewBuffers) kern = rle::encode_kernel<rle::kFewDepth>;
+    auto kern = pol ? rle::encode_kernel<2u, 1u> : rle::encode_kernel<2u, 2u>;
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kEncWaves)), dim3(rle::kEncBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_status, n,
                        pol | flags);
@@ -1036,23 +779,14 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return RLE_E_INVAL;
     if (n > kMaxGrid) return RLE_E_INVAL;
     const hipStream_t s = (hipStream_t)stream;
-    // more buffers than one residency round: issue them longest first (rle::dec_order_kernel)
-    constexpr size_t kOrderExtra = RLE_ORDER_LOCAL ? 0u : 2u * rle::kOrderBuckets;
-    OrderArray oa;   // [n] issue order, then [kOrderBuckets] counts and cursors
-    const size_t entry = RLE_ORDER_DESC && RLE_ORDER_LOCAL ? sizeof(rle::OrderDesc) : sizeof(uint32_t);
-    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, entry * (size_t)n + sizeof(uint32_t) * kOrderExtra);
+    // more buffers than one residency round: issue them longest first (rle::dec_order_local_kernel,
+    // one launch of chunk-local sorts into the [n] issue-order array)
+    OrderArray oa;
+    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, sizeof(uint32_t) * (size_t)n);
     uint32_t* order = oa.p;
-    if (order && RLE_ORDER_LOCAL) {   // one launch, chunk-local sorts (rle::dec_order_local_kernel)
+    if (order)
         hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
-                           s, d_in_len, n, order, rle::OrderMeta{d_in_off, d_out_off, d_out_len, d_out_cap});
-    } else if (order) {
-        uint32_t* hist = order + n;
-        uint32_t* cursor = hist + rle::kOrderBuckets;
-        const dim3 g((n + rle::kOrderChunk - 1u) / rle::kOrderChunk);
-        if (hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2u * rle::kOrderBuckets, s) != hipSuccess) return RLE_E_HIP;
-        hipLaunchKernelGGL(rle::dec_order_hist_kernel, g, dim3(256), 0, s, d_in_len, n, hist);
-        hipLaunchKernelGGL(rle::dec_order_scatter_kernel, g, dim3(256), 0, s, d_in_len, n, hist, cursor, order);
-    }
+                           s, d_in_len, n, order);
     const uint32_t pol = store_policy(n, false);
     const int rw = g_dec_round.load(std::memory_order_relaxed);
     if (n > kDecRound && rw != 0 && max_in_len >= kRoundMinIn) {   // rounds of rw tiles per buffer
@@ -1069,11 +803,8 @@ int decode_launch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_
     // past one residency round of the one-pass staging, the smaller staging (more waves per SIMD);
     // a few buffers (single drop-in calls): the deep tile ring
     const bool large = n > kDecRound && kDecChunksLarge != rle::kDecChunks;
-    auto kern = !RLE_WT_STATIC ? (large ? rle::decode_kernel<kDecChunksLarge> : rle::decode_kernel<rle::kDecChunks>)
-                : large ? (pol ? rle::decode_kernel<kDecChunksLarge, 0u, 1u> : rle::decode_kernel<kDecChunksLarge, 0u, 2u>)
-                        : (pol ? rle::decode_kernel<rle::kDecChunks, 0u, 1u> : rle::decode_kernel<rle::kDecChunks, 0u, 2u>);
-    if constexpr (rle::kFewDepth > 2u)
-        if (n <= kFewBuffers) kern = rle::decode_kernel<rle::kDecChunks, rle::kFewDepth>;
+    auto kern = large ? (pol ? rle::decode_kernel<kDecChunksLarge, 0u, 1u> : rle::decode_kernel<kDecChunksLarge, 0u, 2u>)
+                      : (pol ? rle::decode_kernel<rle::kDecChunks, 0u, 1u> : rle::decode_kernel<rle::kDecChunks, 0u, 2u>);
     hipLaunchKernelGGL(kern, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, d_out_cap,
                        d_status, n, pol | flags, (const uint32_t*)order);
@@ -1179,12 +910,11 @@ extern "C" int rle_decode_pattern_device(const void* d_in, const uint64_t* d_in_
     if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len || n > kMaxGrid) return RLE_E_INVAL;
     const hipStream_t s = (hipStream_t)stream;
     OrderArray oa;   // the decode's issue order (decode_launch)
-    const size_t entry = RLE_ORDER_DESC ? sizeof(rle::OrderDesc) : sizeof(uint32_t);
-    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, entry * (size_t)n);
+    if (n > kDecRound && dec_order_enabled()) order_acquire(oa, s, sizeof(uint32_t) * (size_t)n);
     uint32_t* order = oa.p;
     if (order)
         hipLaunchKernelGGL(rle::dec_order_local_kernel, dim3((n + rle::kLocalChunk - 1u) / rle::kLocalChunk), dim3(256), 0,
-                           s, d_in_len, n, order, rle::OrderMeta{d_in_off, d_out_off, d_out_len, nullptr});
+                           s, d_in_len, n, order);
     hipLaunchKernelGGL(rle::pattern_kernel, dim3(grid_for(n, rle::kDecWaves)), dim3(rle::kDecBlock), 0, s,
                        (const uint8_t*)d_in, d_in_off, d_in_len, (uint8_t*)d_out, d_out_off, d_out_len, n,
                        (const uint32_t*)order);

@@ -59,7 +59,7 @@ __device__ __forceinline__ u32 round_fill(u32 v, u32 ttot, u32 lane, u32x4 rso, 
 }
 
 // Phase C, literal tiles (dec_lit_an's analysis f): each lane's kept bytes as one 16-byte store at
-// its offset (dec_lit_emit), clipped at ttot, then the tile's last 4 bytes as one dword ending at
+// its offset (the compaction of dec_tile_fast), clipped at ttot, then the tile's last 4 bytes as one dword ending at
 // ttot (dec_tile_fast's tail form).  ttot >= 16.
 __device__ __forceinline__ u32 round_lit(const DecPrep& pr, const DecLit& f, u32 lane, const u32x4* clut, u32x4 rso,
                                          u32 ttot, bool wt) {
@@ -164,9 +164,6 @@ __device__ __forceinline__ u32 round_gen(const DecPrep& pr, const DecLen& ln, u3
     return rounds;
 }
 
-#ifndef RLE_ROUND_UNI   // the uniform-tile test after a single-value tile of the same wave
-#define RLE_ROUND_UNI 1
-#endif
 
 #ifndef RLE_ROUND_WPE   // waves per SIMD the register allocation must allow (7: <= 72 VGPRs, the
 #define RLE_ROUND_WPE 7     // 7 four-wave workgroups per CU the LDS allows)
@@ -272,11 +269,12 @@ __global__ __launch_bounds__(kWave* kW) __attribute__((amdgpu_waves_per_eu(RLE_R
         DecLit lit{};
         DecLen ln{};
         if (act) {
-            if (RLE_ROUND_UNI && RLE_DEC_UNIFORM && sv && pos + kSlot + 2u <= C && dec_uniform_tile(cur, lane, kc.LM3, d, v)) {
+            // (the uniform test after a single-value tile of the same wave, as dec_tile's gate)
+            if (sv && pos + kSlot + 2u <= C && dec_uniform_tile(cur, lane, kc.LM3, d, v)) {
                 kind = kTileUni;
                 ttot = kUniformOut;
             }
-            if (kind == kTileNone && RLE_DEC_FAST && !pr.tail) {
+            if (kind == kTileNone && !pr.tail) {
                 const u32 NE16 = (pr.xa >> 7) | (pr.xb << 1);
                 if (!(__builtin_amdgcn_ballot_w64(__builtin_popcount(~NE16 & 0xFFFFu) > 2) & kOwned)) {
                     lit = dec_lit_an(pr, lane, d);
@@ -302,7 +300,7 @@ __global__ __launch_bounds__(kWave* kW) __attribute__((amdgpu_waves_per_eu(RLE_R
                 }
                 kind = kTileGen;
                 // a tile whose tokens all carry one byte (zero-filled data past the uniform test)
-                if (RLE_DEC_FAST && 7u * ttot >= 20u * (C - pos < kTileStep ? C - pos : kTileStep)) {
+                if (7u * ttot >= 20u * (C - pos < kTileStep ? C - pos : kTileStep)) {
                     const u32 vt = (readlane(pr.w[0], 0) >> (8u * d)) & 0xFFu;
                     const u32 vv = rep4(vt);
                     u32 bd = 0;

@@ -40,18 +40,10 @@ constexpr u32 kNone = 0xFFFFFFFFu;
 // per-buffer flags (workspace) written by the scans, read by the writers
 constexpr u32 kFlagSkip = 1u;     // bad buffer: status already written
 constexpr u32 kFlagSerial = 2u;   // decode: the exact serial path handles the whole buffer
-#ifndef RLE_SEG_FAST   // the write passes take the fast tile paths (round 3); 0: general path only
-#define RLE_SEG_FAST 1
-#endif
-#ifndef RLE_SEG_REVERSE   // the write passes take the segments last-summarised first (memory-side cache reuse)
-#define RLE_SEG_REVERSE 1   // r3w, same process: configs[2] mixed batch encode -6 %, decode -2 %; 1 MiB kinds +-1 %
-#endif
-#ifndef RLE_SEG_SUMDEFER   // 1: a decode summary sums its lanes' counts once per segment, not per tile
-#define RLE_SEG_SUMDEFER 1
-#endif
-#ifndef RLE_SEG_SUMFAST   // the summaries count uniform / literal tiles without the full analysis (round 3)
-#define RLE_SEG_SUMFAST 1
-#endif
+// The write passes take the fast tile paths (round 3) and the segments last-summarised first
+// (memory-side cache reuse; r3w, same process: configs[2] mixed batch encode -6 %, decode -2 %, 1 MiB
+// kinds +-1 %); the summaries count uniform / literal tiles without the full analysis (round 3) and
+// sum their lanes' counts once per segment, not per tile (round 5).
 
 // Segments of an n-byte buffer: n = q S + r gives q + (r >= 3) segments (at least one); the last
 // absorbs a remainder of 1-2 bytes, so a stream's final token never starts a segment of its own.
@@ -125,10 +117,7 @@ __global__ __launch_bounds__(kMapBlock) void seg_map_kernel(const u32* __restric
 }
 // A launch of one buffer (the drop-in's single large calls) skips the plan and map launches: the
 // launcher passes seg_first = seg_buf = nullptr, and every segment is buffer 0's, its segments
-// [0, seg_count(in_len[0])) (RLE_SEG_ONE).
-#ifndef RLE_SEG_ONE
-#define RLE_SEG_ONE 1
-#endif
+// [0, seg_count(in_len[0])) (round 5).
 __device__ __forceinline__ u32 seg_total(const u32* seg_first, u32 n, const uint64_t* len, u32 sb) {
     return seg_first ? uniform(seg_first[n]) : seg_count(len32(len[0]), sb);
 }
@@ -174,10 +163,7 @@ __device__ __forceinline__ bool walk_seg(u32x4 rs, u32 start, u32 ntiles, u32 la
 #endif
 constexpr u32 kResTiles = RLE_RES_TILES;
 constexpr u32 kResBytes = (kResTiles * kTileStep + 16u + 1023u) & ~1023u;
-#ifndef RLE_RES_PAD   // debug: spare LDS bytes after each wave's region
-#define RLE_RES_PAD 0
-#endif
-[[maybe_unused]] constexpr u32 kResStride = kResBytes + RLE_RES_PAD;
+[[maybe_unused]] constexpr u32 kResStride = kResBytes;
 #ifndef RLE_RES_DEC_CHUNKS   // the resident decode's staging (chunks per wave; its region takes LDS too)
 #define RLE_RES_DEC_CHUNKS 96
 #endif
@@ -209,7 +195,7 @@ __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u3
     const u32x4 rsi = make_rsrc(src, (U + 15u) & ~15u);
     u32 prev_top = p0 ? (u32)src[p0 - 1u] << 24 : 0u;
     u32 rs = p0, fb = kNone, lb = kNone, rest = 0;
-    u32 restl = 0u, lbl = 0u;   // RLE_SEG_SUMDEFER: the lane's token bytes and its last boundary + 1 (0: none)
+    u32 restl = 0u, lbl = 0u;   // the lane's token bytes and its last boundary + 1 (0: none), summed once per segment
     const EncK kc = enc_k();
     walk_seg<kRes>(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
@@ -217,7 +203,7 @@ __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u3
         const u32 pos = p0 + t * kTileStep;
         // (tried only when the run entering the tile is already 16 bytes long, a scalar test
         // that keeps the check off random and short-run tiles)
-        if (RLE_SEG_SUMFAST && pos != 0u && pos - rs >= 16u && pos + kTileStep < p1) {
+        if (pos != 0u && pos - rs >= 16u && pos + kTileStep < p1) {
             // a tile inside a run (every byte, and the first lookahead byte, equal to the byte
             // before the tile; never the buffer's first tile, whose position 0 is a boundary
             // whatever its byte): no boundary, so fb, lb and rs stay; the tokens count only past
@@ -241,39 +227,26 @@ __device__ __forceinline__ uint4 enc_seg_summarize(const uint8_t* src, u32 U, u3
         const EncAn an = enc_analyze<false>(cur, uint2{0u, 0u}, pos, U, p1, lane, prev_top, rs, kc);
         // run boundaries inside the segment: the first one (L0) and the last one (lb)
         const u32 Bo = an.B & an.validm;
-        if (RLE_SEG_SUMDEFER) {
-            // the first boundary on the scalar unit until found; the last one per lane (tiles come in
-            // order, so a lane's latest is its last), the lanes' maximum taken once per segment
-            if (fb == kNone) {
-                const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
-                if (bl) fb = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), (u32)__builtin_ctzll(bl));
-            }
-            lbl = Bo ? an.p0 + 32u - (u32)__builtin_clz(Bo) : lbl;
-        } else {
+        // the first boundary on the scalar unit until found; the last one per lane (tiles come in
+        // order, so a lane's latest is its last), the lanes' maximum taken once per segment (round 5:
+        // the per-tile wave reductions it replaced measured within +-2 %)
+        if (fb == kNone) {
             const uint64_t bl = __builtin_amdgcn_ballot_w64(Bo != 0u);
-            if (bl) {
-                const u32 fl = (u32)__builtin_ctzll(bl), ll = 63u - (u32)__builtin_clzll(bl);
-                const u32 first = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), fl);
-                const u32 last = readlane(an.p0 + 31u - (u32)__builtin_clz(Bo | 1u), ll);
-                if (fb == kNone) fb = first;
-                lb = last;
-            }
+            if (bl) fb = readlane(an.p0 + (u32)__builtin_ctz(Bo | 0x10000u), (u32)__builtin_ctzll(bl));
         }
+        lbl = Bo ? an.p0 + 32u - (u32)__builtin_clz(Bo) : lbl;
         // tokens at or after the first boundary do not depend on the entering run phase
         u32 fbm = 0u;
         if (fb != kNone) fbm = fb <= an.p0 ? 0xFFFFu : (fb >= an.p0 + 16u ? 0u : ~lowmask(fb - an.p0) & 0xFFFFu);
-        if (RLE_SEG_SUMDEFER) restl += bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u);
-        else rest += wave_sum(bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u));
+        restl += bcnt(an.T & fbm, 0u) + 2u * bcnt(an.P & fbm, 0u);
         prev_top = readlane(an.top, kOwnLanes - 1u);
         const u32 i63 = readlane(an.incl, kOwnLanes - 1u);
         rs = i63 > rs ? i63 : rs;
         return 0u;
     });
-    if (RLE_SEG_SUMDEFER) {
-        rest += wave_sum(restl);
-        const u32 m = readlane(wave_scan_incl(lbl, 0u, OpMax()), kWave - 1u);
-        if (m) lb = m - 1u;
-    }
+    rest += wave_sum(restl);
+    const u32 m = readlane(wave_scan_incl(lbl, 0u, OpMax()), kWave - 1u);
+    if (m) lb = m - 1u;
     const u32 L0 = fb == kNone ? p1 - p0 : fb - p0;
     const u32 cont = (fb == kNone && p1 < U && src[p1] == src[p1 - 1u]) ? 1u : 0u;
     return make_uint4(L0, lb == kNone ? 0u : lb + 1u, rest, cont);
@@ -382,7 +355,7 @@ __device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, 
     walk_seg<kRes>(rsi, p0, ntiles_for(p1 - p0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         // the fast tile paths (round 3; until then only the one-wave kernels took them): past the
         // segment's shared first chunk and before its last tile, as in a one-wave walk
-        return enc_tile<false, RLE_SEG_FAST>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc, elut);
+        return enc_tile<false, true>(cs, nx, p0 + t * kTileStep, U, p1, lane, stage, dst, rso, st, kc, elut);
     });
     // the final partial chunk (< 16 bytes, staging chunk 1): byte stores, nothing past this
     // segment's output and nothing before it
@@ -395,18 +368,8 @@ __device__ __forceinline__ void enc_seg_write(const uint8_t* src, uint8_t* dst, 
 // the last token's count depends on the input, through the (up to 8) run bytes after the segment.
 // Its output is written from that alone, without reading the segment a second time (the summary
 // pass has read it): aligned 16-byte chunks of the 3-periodic pattern, and the partial chunks at
-// both ends, which the neighbouring segments share, bytewise.  (RLE_SEG_UNIFORM; round 3.)
-#ifndef RLE_SEG_UNIFORM
-#define RLE_SEG_UNIFORM 1
-#endif
-#ifndef RLE_SEG_UNIFORM_INLINE
-#define RLE_SEG_UNIFORM_INLINE 0
-#endif
-#if RLE_SEG_UNIFORM_INLINE
-#define RLE_SEG_UNIFORM_ATTR __forceinline__
-#else
+// both ends, which the neighbouring segments share, bytewise.  (Round 3.)
 #define RLE_SEG_UNIFORM_ATTR __attribute__((noinline))   // out of the write loop's hot code (r3x)
-#endif
 __device__ RLE_SEG_UNIFORM_ATTR void enc_seg_uniform(const uint8_t* src, uint8_t* dst, u32 U, u32 p0, u32 p1, u32 rs,
                                                 u32 off, u32 lane) {
     const u32 v = src[p0];
@@ -480,10 +443,10 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
     u32 total = seg_total(seg_first, n, in_len, sb);
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
-        const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
+        const u32 g = total - 1u - g0;
         // (the segment's own plan and summary load with its buffer index, not after it)
         const uint2 pl = plan[g];
-        const uint4 sm = RLE_SEG_UNIFORM ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 sm = summ[g];
         const u32 b = seg_of(seg_buf, g);
         if (uniform(bflag[b])) continue;
         const u32 s0 = seg_lo(seg_first, b), nseg = seg_hi(seg_first, b, in_len, sb) - s0;
@@ -492,7 +455,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
         uint8_t* dst = out + out_off[b];
         u32 p0, p1;
         seg_range(g - s0, nseg, U, sb, p0, p1);
-        if (RLE_SEG_UNIFORM && p0 > 0u) {
+        if (p0 > 0u) {
             if (uniform(sm.y) == 0u && uniform(sm.x) == p1 - p0) {   // no run boundary in the segment
                 enc_seg_uniform(src, dst, U, p0, p1, uniform(pl.x), uniform(pl.y), lane);
                 continue;
@@ -507,9 +470,6 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_write_kernel(const uint8_t*
 // never the product librle_mi355x.so.  VERDICT r3 item 8.)  The fused single-pass encode and the
 // resident single-pass kernels are bit-exact and tested, but slower than the five-launch default
 // ("Round 3: segmented path"), so the product does not carry them.
-#ifndef RLE_VARIANTS
-#define RLE_VARIANTS 0
-#endif
 #if RLE_VARIANTS
 // ---------------------------------------------------------------- fused single-pass encode
 // One launch after the plan (SURVEY.md §5's single-pass form, with a decoupled look-back carry):
@@ -674,14 +634,11 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_fused_kernel(const uint8_t*
 // its whole batch (measured: the look-backs run out of polls).  The next ticket is taken while the
 // current segment is processed, which hides the atomic's latency and keeps progress (a wave's
 // prefetched segment is always later than its current one).
-// RLE_RES_TICKETLESS (default): no ticket counter; wave w of workgroup k takes segment 4 k + w
-// of a grid of one wave per segment.  A workgroup is dispatched only after every lower-numbered
+// Since round 3 without the ticket counter: wave w of workgroup k takes segment 4 k + w of a grid
+// of one wave per segment.  A workgroup is dispatched only after every lower-numbered
 // workgroup of its XCD, so the lowest-numbered waiting segment's predecessors are all running or
 // done, and the look-back cannot wait forever (and its polls are bounded regardless: a wave that
 // runs out marks its buffer and exits).
-#ifndef RLE_RES_TICKETLESS
-#define RLE_RES_TICKETLESS 1
-#endif
 __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len,
@@ -704,14 +661,12 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
-    u32 gnext = 0;
-    if (RLE_RES_TICKETLESS) gnext = blockIdx.x * kSegWaves + wid;   // one segment per wave
-    else if (lane == 0) gnext = atomicAdd(ticket, 1u);
+    (void)ticket;
+    u32 gnext = blockIdx.x * kSegWaves + wid;   // one segment per wave
     for (;;) {
         const u32 g = uniform(gnext);
         if (g >= total) break;
-        if (RLE_RES_TICKETLESS) gnext = total;
-        else if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
+        gnext = total;
         {
             const u32 b = uniform(seg_buf[g]);
             const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
@@ -773,7 +728,7 @@ __global__ __launch_bounds__(kSegBlock) void enc_seg_res_kernel(const uint8_t* _
 // literal path's count, dec_tile_fast, without its stores or its per-lane limits).  kNotFast when a
 // pair has another count (the caller then runs dec_lengths).  About 40 VALU against ~100 for
 // dec_lengths + its sum.
-// kLane: the lane's own count (the caller sums the lanes once per segment, RLE_SEG_SUMDEFER).
+// kLane: the lane's own count (the caller sums the lanes once per segment).
 template <bool kLane = false>
 __device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 lane, const DecK& kc) {
     constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
@@ -830,8 +785,8 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
                                                    const uint8_t* slots, const DecEntry* tbl) {
     const u32x4 rsi = make_rsrc(src, (C + 15u) & ~15u);
     u32 d0 = 0u, d1 = 1u, d2 = 2u, c0 = 0u, c1 = 0u, c2 = 0u, badm = 0u;
-    u32 uni = RLE_SEG_UNIFORM ? 7u : 0u, v0 = 0u, v1 = 0u, v2 = 0u;   // single-byte phases and their bytes
-    u32 accm = 0u;       // RLE_SEG_SUMDEFER: the lane's decoded bytes over the tiles after the phases merged
+    u32 uni = 7u, v0 = 0u, v1 = 0u, v2 = 0u;   // single-byte phases and their bytes
+    u32 accm = 0u;       // the lane's decoded bytes over the tiles after the phases merged (summed once)
     bool badl = false;   // ... and whether the lane declined in one of them
     const DecK kc = dec_k();
     walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
@@ -840,17 +795,12 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
         const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
         const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
         if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
-            u32 tot = (RLE_SEG_SUMFAST && !pr.tail) ? dec_count_literal<RLE_SEG_SUMDEFER>(pr, d0, lane, kc) : kNotFast;
-            bool bad = false;
+            u32 tot = !pr.tail ? dec_count_literal<true>(pr, d0, lane, kc) : kNotFast;
             if (tot == kNotFast) {
                 const DecLen ln = dec_lengths(pr, d0);
-                if (RLE_SEG_SUMDEFER) {   // the lane's count and decline, summed once per segment
-                    tot = lane < kOwnLanes ? ln.nout : 0u;
-                    badl |= lane < kOwnLanes && ln.serial_lane;
-                } else {
-                    tot = owned_sum(ln.nout);
-                    bad = owned_any(ln.serial_lane);
-                }
+                // the lane's count and decline, summed once per segment
+                tot = lane < kOwnLanes ? ln.nout : 0u;
+                badl |= lane < kOwnLanes && ln.serial_lane;
                 if (uni) {
                     u32 v;
                     const bool one = dec_tile_single(pr, ln, d0, kc, v);
@@ -861,12 +811,7 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
             } else {
                 uni = 0u;   // a literal tile (its own bytes, "v v 2" pairs): not counted as single-byte
             }
-            if (RLE_SEG_SUMDEFER) {
-                accm += tot;
-            } else {
-                c0 += tot; c1 += tot; c2 += tot;
-                badm |= bad ? 7u : 0u;
-            }
+            accm += tot;
             d0 = d1 = d2 = bfe(m63, 8u * d0, 8);
         } else {
             const DecLen l0 = dec_lengths(pr, d0);
@@ -896,11 +841,9 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
         }
         return 0u;
     });
-    if (RLE_SEG_SUMDEFER) {
-        const u32 cm = wave_sum(accm);
-        c0 += cm; c1 += cm; c2 += cm;
-        badm |= __builtin_amdgcn_ballot_w64(badl) ? 7u : 0u;
-    }
+    const u32 cm = wave_sum(accm);
+    c0 += cm; c1 += cm; c2 += cm;
+    badm |= __builtin_amdgcn_ballot_w64(badl) ? 7u : 0u;
     return make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8) | (uni << 11));
 }
 // the summary of an empty stream: counts 0, exit = entry
@@ -1031,7 +974,7 @@ __device__ __forceinline__ void dec_seg_write(const uint8_t* src, uint8_t* dst, 
     const bool serial = walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         // the fast tile paths (round 3): past the segment's shared first chunk, and the literal
         // path only on tiles a later tile of this segment follows (dec_tile)
-        return dec_tile<RLE_SEG_FAST, kChunks, false>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc,
+        return dec_tile<true, kChunks, false>(cs, nx, q0 + t * kTileStep, C, q1, U, lane, tbl, stage, dst, rso, st, kc,
                                                clut);
     });
     dec_finish(st, last ? U : st.out_pos, lane, stage, rso, dst);
@@ -1070,9 +1013,9 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
     u32 total = seg_total(seg_first, n, in_len, sb);
     total = total < maxseg ? total : maxseg;
     for (u32 g0 = blockIdx.x * kSegWaves + wid; g0 < total; g0 += gridDim.x * kSegWaves) {
-        const u32 g = RLE_SEG_REVERSE ? total - 1u - g0 : g0;
+        const u32 g = total - 1u - g0;
         const uint2 pl = plan[g];
-        const uint4 sm = RLE_SEG_UNIFORM ? summ[g] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 sm = summ[g];
         const u32 b = seg_of(seg_buf, g);
         const u32 flag = uniform(bflag[b]);
         if (flag & kFlagSkip) continue;
@@ -1090,7 +1033,7 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_write_kernel(const uint8_t*
         }
         u32 q0, q1;
         seg_range(g - s0, nseg, C, sb, q0, q1);
-        if (RLE_SEG_UNIFORM && g + 1u != s0 + nseg) {   // one byte throughout: no second read
+        if (g + 1u != s0 + nseg) {   // one byte throughout: no second read
             const u32 e = uniform(pl.x);
             if ((uniform(sm.w) >> (11u + e)) & 1u) {
                 const u32 cnt = uniform(e == 0u ? sm.x : (e == 1u ? sm.y : sm.z));
@@ -1148,14 +1091,12 @@ __global__ __launch_bounds__(kSegBlock) void dec_seg_res_kernel(const uint8_t* _
     __syncthreads();
     u32 total = uniform(seg_first[n]);
     total = total < maxseg ? total : maxseg;
-    u32 gnext = 0;
-    if (RLE_RES_TICKETLESS) gnext = blockIdx.x * kSegWaves + wid;   // one segment per wave
-    else if (lane == 0) gnext = atomicAdd(ticket, 1u);
+    (void)ticket;
+    u32 gnext = blockIdx.x * kSegWaves + wid;   // one segment per wave
     for (;;) {
         const u32 g = uniform(gnext);
         if (g >= total) break;
-        if (RLE_RES_TICKETLESS) gnext = total;
-        else if (lane == 0) gnext = atomicAdd(ticket, 1u);   // the next ticket, while this one is processed
+        gnext = total;
         {
             const u32 b = uniform(seg_buf[g]);
             const u32 s0 = uniform(seg_first[b]), s1 = uniform(seg_first[b + 1]), nseg = s1 - s0;
@@ -1299,31 +1240,24 @@ int device_cus(int* ncu) {
     return RLE_OK;
 }
 // segment length in bytes: about 16 segments per CU over the batch, 4..16 tiles each
-// (RLE_SEG_TILES_FIX > 0: a fixed segment length, for A/B builds)
-#ifndef RLE_SEG_TILES_FIX
-#define RLE_SEG_TILES_FIX 0
-#endif
+// (longer segments, caps of 32 / 64 tiles, measured slower on the mixed batch: r5w)
 // The resident single-pass kernels (enc_seg_res_kernel / dec_seg_res_kernel): RLE_MI355X_SEG_RES=1|0
 // overrides the build default.  Their segments are one tile shorter than an LDS region, so that a
 // buffer's last segment (which absorbs a remainder of up to 2 bytes) still fits.  Segment lengths
 // stay whole tiles: a segment's exit state is read after the last tile's last lane (an 8048-byte
 // segment, measured, left the decode exit phase one lane late).
-#ifndef RLE_SEG_RES_DEFAULT
-#define RLE_SEG_RES_DEFAULT 0
-#endif
 // 0 off, 1 the resident single pass, 2 the single pass without the resident segment (decode)
 int seg_res_mode() {
     if (!RLE_VARIANTS) return 0;   // (product build: RLE_MI355X_SEG_RES is not read)
     static const int m = [] {
         const char* e = getenv("RLE_MI355X_SEG_RES");
-        return e ? atoi(e) : RLE_SEG_RES_DEFAULT;
+        return e ? atoi(e) : 0;
     }();
     return m;
 }
 bool seg_res() { return seg_res_mode() == 1; }
 inline uint32_t seg_bytes(uint64_t total, int ncu) {
     if (seg_res()) return (rle::kResTiles - 1u) * rle::kTileStep;
-    if (RLE_SEG_TILES_FIX) return (uint32_t)RLE_SEG_TILES_FIX * rle::kTileStep;
     const uint64_t tiles = (total + rle::kTileStep - 1) / rle::kTileStep;
     uint64_t per = tiles / ((uint64_t)ncu * 16u);
     per = per < rle::kSegTilesMin ? rle::kSegTilesMin : (per > rle::kSegTilesMax ? rle::kSegTilesMax : per);
@@ -1343,14 +1277,11 @@ inline uint32_t seg_grid(uint32_t maxseg, int ncu) {
 inline uint32_t map_grid(uint32_t maxseg) { return (maxseg + rle::kMapBlock - 1) / rle::kMapBlock; }
 inline uint32_t buf_grid(uint32_t n) { return (n + rle::kSegWaves - 1) / rle::kSegWaves; }
 // the fused single-pass encode (RLE_MI355X_SEG_FUSED=1; measured slower than the four launches, §4)
-#ifndef RLE_SEG_FUSED_DEFAULT
-#define RLE_SEG_FUSED_DEFAULT 0
-#endif
 [[maybe_unused]] bool seg_fused() {
     if (!RLE_VARIANTS) return false;   // (product build: RLE_MI355X_SEG_FUSED is not read)
     static const bool on = [] {
         const char* e = getenv("RLE_MI355X_SEG_FUSED");
-        return e ? e[0] != '0' : RLE_SEG_FUSED_DEFAULT != 0;
+        return e ? e[0] != '0' : false;
     }();
     return on;
 }
@@ -1384,7 +1315,7 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
                            maxseg, w.ticket, d_status);
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
-        hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
+        hipLaunchKernelGGL(rle::enc_seg_res_kernel, dim3(buf_grid(maxseg)),
                            dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_status, n, w.seg_first, w.seg_buf, maxseg,
                            sb, w.summ, w.incl, w.sflag, w.ticket);
@@ -1400,8 +1331,8 @@ extern "C" int rle_encode_batch_device_seg(const void* d_in, const uint64_t* d_i
     }
 #endif
     const uint32_t grid = seg_grid(maxseg, ncu);
-    // one buffer: no plan / map launches, the kernels take its segments from its length (RLE_SEG_ONE)
-    const bool one = RLE_SEG_ONE && n == 1u;
+    // one buffer: no plan / map launches, the kernels take its segments from its length
+    const bool one = n == 1u;
     uint32_t* const seg_first = one ? nullptr : w.seg_first;
     uint32_t* const seg_buf = one ? nullptr : w.seg_buf;
     if (!one) {
@@ -1442,7 +1373,7 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
         hipLaunchKernelGGL(rle::seg_map_kernel, dim3(map_grid(maxseg)), dim3(rle::kMapBlock), 0, s, w.seg_first, n,
                            maxseg, w.seg_buf);
         hipLaunchKernelGGL(seg_res_mode() == 1 ? rle::dec_seg_res_kernel<true> : rle::dec_seg_res_kernel<false>,
-                           dim3(RLE_RES_TICKETLESS ? buf_grid(maxseg) : seg_grid(maxseg, ncu)),
+                           dim3(buf_grid(maxseg)),
                            dim3(rle::kSegBlock), 0, s, in,
                            d_in_off, d_in_len, out, d_out_off, d_out_len, d_out_cap, d_status, n, w.seg_first,
                            w.seg_buf, maxseg, sb, w.summ, w.incl, w.sflag, w.ticket, w.bflag);
@@ -1452,7 +1383,7 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
     }
 #endif
     const uint32_t grid = seg_grid(maxseg, ncu);
-    const bool one = RLE_SEG_ONE && n == 1u;   // (as in the encode: no plan / map launches for one buffer)
+    const bool one = n == 1u;   // (as in the encode: no plan / map launches for one buffer)
     uint32_t* const seg_first = one ? nullptr : w.seg_first;
     uint32_t* const seg_buf = one ? nullptr : w.seg_buf;
     if (!one) {
@@ -1465,11 +1396,7 @@ extern "C" int rle_decode_batch_device_seg(const void* d_in, const uint64_t* d_i
                        seg_first, seg_buf, maxseg, sb, w.summ);
     hipLaunchKernelGGL(rle::dec_seg_scan_kernel, dim3(buf_grid(n)), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len,
                        out, d_out_off, d_out_len, d_out_cap, d_status, n, seg_first, maxseg, sb, w.summ, w.plan, w.bflag);
-#ifndef RLE_SEG_DEC_FORCE   // A/B builds: 96 or 192 forces the decode write pass's staging
-#define RLE_SEG_DEC_FORCE 0
-#endif
-    const bool one_round = RLE_SEG_DEC_FORCE ? RLE_SEG_DEC_FORCE == 192
-                                             : maxseg <= (uint32_t)ncu * 16u;   // the 192-chunk kernel's residency
+    const bool one_round = maxseg <= (uint32_t)ncu * 16u;   // the 192-chunk kernel's residency
     hipLaunchKernelGGL(one_round ? rle::dec_seg_write_kernel<rle::kSegDecChunksOne>
                                  : rle::dec_seg_write_kernel<rle::kSegDecChunksMany>,
                        dim3(grid), dim3(rle::kSegBlock), 0, s, in, d_in_off, d_in_len, out, d_out_off, d_out_len,
