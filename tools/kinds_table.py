@@ -2,7 +2,9 @@
 """Per-kind roofline table of the 64 KiB decode / encode (the north-star batch and its four data
 kinds) from a tools/gpu_kinds.sh run: rocprof median kernel time per workload, the batch's
 algorithmic bytes (U + C, C from the oracle's encoding of the same seeded buffers), GB/s and the
-fraction of 8 TB/s.   usage: python tools/kinds_table.py gpurun_out/<tag>_kinds > profiles/<tag>_kinds.md"""
+fraction of 8 TB/s.  --skip K drops each kernel's first K launches (round 6: the warm launches of
+tools/gpu_kinds.sh, so the table is steady state like bench.py's north-star timing).
+   usage: python tools/kinds_table.py gpurun_out/<tag>_kinds [--skip K] > profiles/<tag>_kinds.md"""
 import collections
 import csv
 import glob
@@ -23,7 +25,9 @@ def c_bytes(kinds):
 
 def main():
     d = sys.argv[1]
-    print(f"# Per-kind 64 KiB codec launches ({os.path.basename(d.rstrip('/'))}, rocprofv3 --kernel-trace, median of 5-6 launches)\n")
+    skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
+    print(f"# Per-kind 64 KiB codec launches ({os.path.basename(d.rstrip('/'))}, rocprofv3 --kernel-trace, "
+          f"median of each kernel's launches after its first {skip})\n")
     print("16384 x 64 KiB per launch (1 GiB of U). Algorithmic bytes = U + C; fraction of 8 TB/s. "
           "Decode excludes the issue-order sort (its own launch, listed).\n")
     print("| workload | C MB | encode µs | encode frac | decode µs | decode frac | sort µs |")
@@ -39,7 +43,7 @@ def main():
                 "sort" if "dec_order" in name else None
             if key:
                 dur[key + name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
-        med = lambda v: sorted(v)[len(v) // 2]
+        med = lambda v: sorted(v[skip:] if len(v) > skip else v)[len(v[skip:] if len(v) > skip else v) // 2]
         enc = [med(v) for k, v in dur.items() if k.startswith("enc")][0]
         dec = [med(v) for k, v in dur.items() if k.startswith("dec") and "decode_kernel" in k][0]
         srt = sum(med(v) for k, v in dur.items() if k.startswith("sort"))
