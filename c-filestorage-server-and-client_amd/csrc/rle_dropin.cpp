@@ -9,8 +9,10 @@
 // hook in the server, src/server.c:406-524) and released at thread exit.  A call is one batched
 // kernel launch with B = 1 plus the host<->device traffic, sized to the call:
 //   small (one wave walks it)  zero-copy on the thread's mapped pinned buffer, one launch, one sync;
-//   medium                     one H2D / one D2H through pinned staging, segmented kernels;
-//   large (>= 256 KiB)         the runtime copies straight from / to the caller's memory.
+//   medium (up to 256 KiB)     zero-copy too: cooperative or segmented kernels on the mapped buffer;
+//   large                      the caller's buffer and the result block registered for the call, one
+//                              DMA in, segmented kernels, one copy kernel out (else the runtime's
+//                              pageable copies or the pinned staging).
 // The result is a fresh malloc() block, which is what the callers free() (src/filesystemApi.c:208,
 // 687, 775, 811; src/server.c:269, 320).  There is no CPU codec in this library: without a
 // usable GPU it reports the problem and aborts.  RLEappend / RLEdecompressN (include/
@@ -62,6 +64,7 @@ struct Stats {
     std::atomic<uint64_t> bytes_h2d{0}, bytes_d2h{0};
     std::atomic<uint64_t> ns_stage_in{0}, ns_device{0}, ns_stage_out{0};
     std::atomic<uint64_t> calls_coalesced{0}, launches_coalesced{0};   // zero-copy calls / their combined launches
+    std::atomic<uint64_t> calls_registered{0}, calls_reg_fallback{0};  // registered large calls / staged instead
 } g_stats;
 inline uint64_t now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -172,6 +175,127 @@ constexpr size_t kZcIn = 0, kZcWords = (size_t)RLE_ZC_IN_KIB << 10, kZcOut = kZc
                  kZcBytes = kZcOut + (kZcWords * 3 / 2 > (204u << 10) ? kZcWords * 3 / 2 : (204u << 10));
 static_assert(kZcWords >= rle::kCoopDecMaxIn, "zero-copy input region");
 constexpr size_t kZcMaxIn = kZcWords, kZcMaxOut = kZcBytes - kZcOut;   // one zero-copy call's bytes
+
+// Registered large calls (profiles/r6j_hostpath_reg.txt, r6_hostpath.md): from
+// g_reg_min bytes (RLE_MI355X_REG_MIN; 0 = never; by default the sizes past the zero-copy calls'
+// reach) an RLEcompress / RLEdecompress registers the caller's input and the result block with the
+// runtime for the duration of the call (hipHostRegister + unregister of 1 MiB of touched heap
+// memory: 0.9 + 0.3 µs).  The input travels by one DMA straight from the caller's pages, the kernels
+// work in device memory, and a copy kernel stores the result into the registered block over PCIe
+// (the write pass storing there itself measured slower: its partial lines, r6k): no CPU copy either
+// way, and a compress reads its output length on the device instead of a second round trip.  1 MiB:
+// 83-89 µs per call against 111-140 through the runtime's pageable copies.
+//
+// Only a call that is the only large call in flight registers (LargeCall): registered calls from
+// several threads at once measured slower than the pageable copies (r6p: 8 threads, 1 MiB round
+// trips, 6.9 against 13.4 GB/s in round 5), and a registration must never meet a pageable copy of
+// the same pages by the runtime (another thread's call on the same stored file), whose pinning in
+// place races the unregistration (r6q: a crash).  So the decision is taken under g_reg_mu together
+// with the count of large calls in flight (no registration starts while another large call is in
+// flight), and a transfer whose caller pages meet a live registration's pages goes through the
+// pinned staging, never handing the runtime that pointer (live_pages).
+size_t g_reg_min = kZcMaxIn + 1;   // (past the zero-copy calls: r6m / r6o)
+std::mutex g_reg_mu;
+std::atomic<int> g_large_calls{0};       // large calls in flight (changed under g_reg_mu)
+// ... and when two last overlapped: a call registers only when none has overlapped it for
+// kRegQuietNs (RLE_MI355X_REG_QUIET_US).  Under a steady multi-threaded load the registering calls
+// that happen to run alone still cost the others (their registration and unregistration), 4
+// threads of 1 MiB round trips 7.5-7.8 against 8.7-9.4 GB/s (r6t).
+std::atomic<uint64_t> g_last_overlap_ns{0};
+uint64_t g_reg_quiet_ns = 2000000;
+// Whether a call starting now would register (read without the lock: a hint, so that a call that
+// will not register does not allocate its worst-case result block first).
+bool reg_likely() {
+    return g_large_calls.load(std::memory_order_relaxed) == 0 &&
+           now_ns() - g_last_overlap_ns.load(std::memory_order_relaxed) > g_reg_quiet_ns;
+}
+int g_live_regs = 0;                     // registrations alive (under g_reg_mu)
+uintptr_t g_live_lo[2], g_live_hi[2];    // the registered call's page spans (under g_reg_mu)
+inline uintptr_t page_lo(const void* p) { return (uintptr_t)p & ~(uintptr_t)4095; }
+inline uintptr_t page_hi(const void* p, size_t n) { return ((uintptr_t)p + n + 4095) & ~(uintptr_t)4095; }
+// Whether host bytes [p, p + n) share a page with a live registration.
+bool live_pages(const void* p, size_t n) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    const uintptr_t lo = page_lo(p), hi = page_hi(p, n);
+    for (int i = 0; i < g_live_regs; ++i)
+        if (lo < g_live_hi[i] && g_live_lo[i] < hi) return true;
+    return false;
+}
+
+// hipHostRegister of [p, p + n) and its device address (nullptr: not registered).  Under g_reg_mu.
+uint8_t* reg_one(const void* p, size_t n, bool read_only) {
+    void* q = const_cast<void*>(p);
+    hipError_t e = hipHostRegister(q, n, hipHostRegisterMapped | (read_only ? hipHostRegisterReadOnly : 0u));
+    if (e != hipSuccess && read_only) {   // (read-only pages that the flag is not supported for)
+        (void)hipGetLastError();
+        e = hipHostRegister(q, n, hipHostRegisterMapped);
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    void* d = nullptr;
+    // (the result block's device address must be 16-byte aligned for the copy kernel; the input
+    // travels by DMA from its host address)
+    if (hipHostGetDevicePointer(&d, q, 0) != hipSuccess || !d || (!read_only && ((uintptr_t)d & 15u))) {
+        (void)hipGetLastError();
+        (void)hipHostUnregister(q);
+        return nullptr;
+    }
+    g_live_lo[g_live_regs] = page_lo(p);
+    g_live_hi[g_live_regs] = page_hi(p, n);
+    ++g_live_regs;
+    return static_cast<uint8_t*>(d);
+}
+void unreg_all(const void* in, const void* out) {   // (the registered call's two, in that order)
+    (void)hipHostUnregister(const_cast<void*>(out));
+    (void)hipHostUnregister(const_cast<void*>(in));
+    (void)hipGetLastError();
+    g_live_regs = 0;
+}
+
+// One drop-in call that moves caller bytes past the zero-copy reach, from before its first
+// transfer to after its last.  Constructed with an input and a result block, it registers both
+// when it is the only large call in flight (registered(); d_in / d_out their device addresses).
+// Leaving, it drains the call's stream before unregistering (a call left by an exception).
+class LargeCall {
+public:
+    explicit LargeCall(hipStream_t s, const void* in = nullptr, size_t n_in = 0, const void* out = nullptr,
+                       size_t n_out = 0)
+        : s_(s) {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        const uint64_t t = now_ns();
+        const int n = ++g_large_calls;
+        if (n > 1) g_last_overlap_ns = t;
+        if (in && n == 1 && t - g_last_overlap_ns > g_reg_quiet_ns && (d_in = reg_one(in, n_in, true))) {
+            if ((d_out = reg_one(out, n_out, false))) {
+                in_ = in;
+                out_ = out;
+            } else {
+                (void)hipHostUnregister(const_cast<void*>(in));
+                (void)hipGetLastError();
+                g_live_regs = 0;
+                d_in = nullptr;
+            }
+        }
+    }
+    ~LargeCall() {
+        if (registered()) (void)hipStreamSynchronize(s_);
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        if (registered()) unreg_all(in_, out_);
+        --g_large_calls;
+    }
+    LargeCall(const LargeCall&) = delete;
+    LargeCall& operator=(const LargeCall&) = delete;
+    bool registered() const { return d_out != nullptr; }
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+
+private:
+    hipStream_t s_;
+    const void* in_ = nullptr;
+    const void* out_ = nullptr;
+};
 
 // Pinned staging of RLEdecompressN is bounded: a batch is processed in chunks of at most this many
 // staged input (and output) bytes, and a file larger than that is copied straight from / to the
@@ -312,6 +436,8 @@ void init_once() {
 #if RLE_TEST_HOOKS
     if (const char* e = getenv("RLE_MI355X_FAIL_ALLOC_ABOVE")) g_fail_above = (size_t)strtoull(e, nullptr, 10);
 #endif
+    if (const char* e = getenv("RLE_MI355X_REG_MIN")) g_reg_min = (size_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("RLE_MI355X_REG_QUIET_US")) g_reg_quiet_ns = 1000ull * strtoull(e, nullptr, 10);
     if (const char* e = getenv("RLE_MI355X_STAGE_CAP")) {
         const long long v = atoll(e);
         if (v >= 16) g_stage_cap = (size_t)v;
@@ -738,14 +864,17 @@ size_t pipe_chunk(size_t n) {
 }
 
 // Whether to_device copies n bytes through the pinned staging (else straight from the caller).
-bool staged(size_t n) { return n > 0 && !(g_staging == Staging::Direct && n >= kPipeMinBytes); }
+bool direct(const void* p, size_t n) {
+    return g_staging == Staging::Direct && n >= kPipeMinBytes && !live_pages(p, n);
+}
+bool staged(const void* p, size_t n) { return n > 0 && !direct(p, n); }
 
 // Queues the copy of n caller bytes at src to d_dst on c->s, staged (when staged) at h_in + hoff;
 // src may be reused on return.  Callers queuing several copies grow h_in for all of them first.
 void to_device(Ctx* c, uint8_t* d_dst, const void* src, size_t n, size_t hoff = 0) {
     const uint8_t* p = static_cast<const uint8_t*>(src);
     if (n == 0) return;
-    if (g_staging == Staging::Direct && n >= kPipeMinBytes) {
+    if (direct(p, n)) {
         check(hipMemcpyAsync(d_dst, p, n, hipMemcpyHostToDevice, c->s), "H2D");
         return;
     }
@@ -767,7 +896,7 @@ void from_device(Ctx* c, void* dst, const uint8_t* d_src, size_t n) {
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
         return;
     }
-    if (g_staging == Staging::Direct && n >= kPipeMinBytes) {
+    if (direct(q, n)) {
         check(hipMemcpyAsync(q, d_src, n, hipMemcpyDeviceToHost, c->s), "D2H");
         check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
         return;
@@ -1295,6 +1424,7 @@ void warm_small(Ctx* c) {
     free(r);
 }
 void warm(Ctx* c) {
+    const LargeCall lc(c->s);   // (its own buffers; a registration elsewhere only stages its copies)
     constexpr size_t kBig = kPipeMinBytes + (64u << 10), kMed = 64u << 10, kSmall = 4096;
     std::vector<uint8_t> buf(kBig), back(kBig);
     for (size_t i = 0; i < kBig; ++i) buf[i] = (uint8_t)(((i * 2654435761u) >> 13) & 3u);   // short runs
@@ -1315,8 +1445,10 @@ void warm(Ctx* c) {
     C = fetch_encoded(c, one_trip, 0);
     queue_decode(c, c->d_out, C, c->d_mid, kMed, kMed);
     from_device(c, out, c->d_mid, kMed);
-    check(hipMemcpyAsync(c->d_in, b, kBig, hipMemcpyHostToDevice, c->s), "H2D");
-    check(hipMemcpyAsync(out, c->d_in, kBig, hipMemcpyDeviceToHost, c->s), "D2H");
+    if (!live_pages(b, kBig) && !live_pages(out, kBig)) {
+        check(hipMemcpyAsync(c->d_in, b, kBig, hipMemcpyHostToDevice, c->s), "H2D");
+        check(hipMemcpyAsync(out, c->d_in, kBig, hipMemcpyDeviceToHost, c->s), "D2H");
+    }
     check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
 }
 
@@ -1324,6 +1456,8 @@ void warm(Ctx* c) {
 
 int rle_append_prepare_launch(const void* d_mid, uint64_t U, void* d_head, unsigned long long* d_start,
                               uint64_t* d_res, hipStream_t s);   // csrc/rle_fileops.hip
+int rle_copy_len_launch(void* dst, const void* src, const uint64_t* d_len, uint64_t max_bytes,
+                        hipStream_t s);                          // csrc/rle_kernels.hip
 
 namespace {
 // RLEappend of a small file (old stream decoded by one wave, c^r ‖ new encoded by one wave, output
@@ -1377,20 +1511,11 @@ bool append_small(Ctx* c, const char* content, size_t C, size_t U, const char* a
 }
 }  // namespace
 
-static char* compress_impl(char* data, size_t U, size_t* compressedSize) {
-    Ctx* c = ctx();
-    // one wave walks it, or (g_zc_seg) the segmented kernels on the mapped buffer: the single-copy path
-    if (U < kSegEncodeBytes || (g_zc_seg && g_zerocopy && U <= kZcMaxIn)) {
-        const uint64_t t0 = now_ns();
-        char* r = compress_small(c, data, U, compressedSize);
-        g_stats.calls_compress++;
-        g_stats.bytes_in += U;
-        g_stats.bytes_out += *compressedSize;
-        g_stats.bytes_h2d += round16(U) + kMetaBytes;
-        g_stats.bytes_d2h += round16(rle_max_compressed_size(U)) + kMetaBytes;
-        g_stats.ns_device += now_ns() - t0;
-        return r;
-    }
+namespace {
+// RLEcompress past the zero-copy reach without registration: the caller's bytes by the runtime's
+// pageable copy (or the pinned staging: live_pages), the tokens back once their count is known.
+// Inside a LargeCall.
+char* compress_large(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     grow_dev(c->d_in, c->d_in_cap, round16(U));
     const uint64_t t0 = now_ns();
     to_device(c, c->d_in, data, U);
@@ -1422,6 +1547,82 @@ static char* compress_impl(char* data, size_t U, size_t* compressedSize) {
     return r;
 }
 
+// Whether an encode of n bytes takes the registered path (g_reg_min; the cooperative kernel's calls
+// stay zero-copy).
+bool registered_encode(size_t n) {
+    return g_reg_min && !g_fake_devs && n >= g_reg_min && n >= kSegEncodeBytes &&
+           !(g_zc_coop && n <= rle::kCoopEncMaxBytes);
+}
+
+// RLEcompress through registered memory (lc registered the caller's U bytes and the result block r
+// of maxC + 16 bytes): the input DMA'd straight from the caller's pages, the tokens copied from
+// device memory into r by the copy kernel, which reads their count on the device.  The device
+// buffers are grown beforehand (compress_impl), so nothing here throws.
+char* compress_registered(Ctx* c, const LargeCall& lc, const char* data, size_t U, char* r, size_t maxC,
+                          size_t* compressedSize) {
+    const uint64_t t0 = now_ns();
+    // launch words in the thread's mapped buffer (as the zero-copy calls'): no copy commands for them,
+    // so the stream is one DMA and four kernels
+    uint64_t* hw = reinterpret_cast<uint64_t*>(c->h_zc + kZcWords);
+    uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+    hw[0] = 0; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = 0;
+    check(hipMemcpyAsync(c->d_in, data, U, hipMemcpyHostToDevice, c->s), "H2D");
+    if (rle_encode_batch_device_seg(c->d_in, dw + 0, dw + 1, c->d_out, dw + 2, dw + 3, reinterpret_cast<uint32_t*>(dw + 4),
+                                    1, U, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
+        die("encode launch", hipGetLastError());
+    if (rle_copy_len_launch(lc.d_out, c->d_out, dw + 3, maxC, c->s) != RLE_OK) die("copy launch", hipGetLastError());
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const size_t C = hw[3];
+    check_encode_status((uint32_t)hw[4]);
+    // The block keeps its worst-case size (the reference's own block is calloc(2U),
+    // src/rleCompression.c:10): shrinking it in place returns the tail to malloc, whose next
+    // worst-case block then comes fresh from the kernel each call (r6l: 1 MiB 521 against 87 µs).
+    memset(r + C, 0, 16);
+    *compressedSize = C;
+    g_stats.calls_registered++;
+    g_stats.calls_compress++;
+    g_stats.bytes_in += U;
+    g_stats.bytes_out += C;
+    g_stats.bytes_h2d += U;
+    g_stats.bytes_d2h += C;
+    g_stats.ns_device += now_ns() - t0;
+    return r;
+}
+}  // namespace
+
+static char* compress_impl(char* data, size_t U, size_t* compressedSize) {
+    Ctx* c = ctx();
+    const bool reg = registered_encode(U) && reg_likely();
+    const bool small = U < kSegEncodeBytes || (g_zc_seg && g_zerocopy && U <= kZcMaxIn);
+    if (reg) {   // the registered path's buffers, grown before anything is registered
+        const size_t maxC = rle_max_compressed_size(U);
+        zc(c);
+        grow_dev(c->d_in, c->d_in_cap, round16(U));
+        grow_dev(c->d_out, c->d_out_cap, round16(maxC));
+        grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, U));
+        char* r = static_cast<char*>(malloc(maxC + 16));
+        if (!r) throw std::bad_alloc();
+        const LargeCall lc(c->s, data, U, r, maxC);
+        if (lc.registered()) return compress_registered(c, lc, data, U, r, maxC, compressedSize);
+        free(r);
+        g_stats.calls_reg_fallback++;
+        if (!small) return compress_large(c, data, U, compressedSize);
+    } else if (!small) {
+        const LargeCall lc(c->s);
+        return compress_large(c, data, U, compressedSize);
+    }
+    // one wave walks it, or (g_zc_seg) the segmented kernels on the mapped buffer: the single-copy path
+    const uint64_t t0 = now_ns();
+    char* r = compress_small(c, data, U, compressedSize);
+    g_stats.calls_compress++;
+    g_stats.bytes_in += U;
+    g_stats.bytes_out += *compressedSize;
+    g_stats.bytes_h2d += round16(U) + kMetaBytes;
+    g_stats.bytes_d2h += round16(rle_max_compressed_size(U)) + kMetaBytes;
+    g_stats.ns_device += now_ns() - t0;
+    return r;
+}
+
 // src/rleCompression.c:9-45 — returns a malloc block: C token bytes + >= 2 zero bytes; NULL (errno
 // = ENOMEM) when an allocation fails, as the reference's calloc can (:10).
 extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize) {
@@ -1440,22 +1641,83 @@ extern "C" char* RLEcompress(char* data, size_t origSize, size_t* compressedSize
     }
 }
 
+namespace {
+// RLEdecompress through registered memory (as compress_registered; lc registered the caller's C
+// bytes and the result block r of U + E bytes): the decoded bytes copied from device memory into r,
+// and for a stream the encoder cannot have written, whatever it put into the E region.
+void decompress_registered(Ctx* c, const LargeCall& lc, const char* data, size_t C, size_t U, size_t E, char* r) {
+    const size_t total = U + E;
+    const uint64_t t0 = now_ns();
+    uint64_t* hw = reinterpret_cast<uint64_t*>(c->h_zc + kZcWords);   // (launch words: compress_registered)
+    uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+    hw[0] = 0; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
+    check(hipMemcpyAsync(c->d_in, data, C, hipMemcpyHostToDevice, c->s), "H2D");
+    uint32_t* d_status = reinterpret_cast<uint32_t*>(dw + 5);
+    const int drc = C >= kSegDecodeBytes
+                        ? rle_decode_batch_device_seg(c->d_in, dw + 0, dw + 1, c->d_out, dw + 2, dw + 3, dw + 4, d_status,
+                                                      1, C, c->d_ws, c->d_ws_cap, c->s)
+                        : rle_decode_batch_device_sized(c->d_in, dw + 0, dw + 1, c->d_out, dw + 2, dw + 3, dw + 4,
+                                                        d_status, 1, C, U, c->s);
+    if (drc != RLE_OK) die("decode launch", hipGetLastError());
+    if (rle_copy_len_launch(lc.d_out, c->d_out, dw + 3, U, c->s) != RLE_OK) die("copy launch", hipGetLastError());
+    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    const uint32_t st = (uint32_t)hw[5];
+    if (E && (st & RLE_STATUS_SERIAL)) {   // a stream the encoder cannot have written may have put bytes
+        // into the E region: they travel too (rare; one more round trip, inside r's registration)
+        check(hipMemcpyAsync(r + U, c->d_out + U, E, hipMemcpyDeviceToHost, c->s), "D2H");
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    } else if (E) {
+        memset(r + U, 0, E);
+    }
+    if (st & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompress");
+    g_stats.calls_registered++;
+    g_stats.calls_decompress++;
+    g_stats.bytes_in += C;
+    g_stats.bytes_out += total;
+    g_stats.bytes_h2d += C;
+    g_stats.bytes_d2h += U;
+    g_stats.ns_device += now_ns() - t0;
+}
+
+// RLEdecompress past the zero-copy reach without registration (as compress_large).  Inside a
+// LargeCall.
+void decompress_large(Ctx* c, const char* data, size_t C, size_t U, size_t E, char* r);   // below
+}  // namespace
+
 static void decompress_impl(char* data, size_t C, size_t U, size_t E, char* r) {
     const size_t total = U + E;
     Ctx* c = ctx();
-    // one wave walks it, or (g_zc_seg) the segmented kernels on the mapped buffer: the single-copy path
-    if ((C < kSegDecodeBytes && total <= kOneTripBytes) ||
-        (g_zc_seg && g_zerocopy && C <= kZcMaxIn && total <= kZcMaxOut)) {
-        const uint64_t t0 = now_ns();
-        decompress_small(c, data, C, U, E, r);
-        g_stats.calls_decompress++;
-        g_stats.bytes_in += C;
-        g_stats.bytes_out += total;
-        g_stats.bytes_h2d += round16(C) + kMetaBytes;
-        g_stats.bytes_d2h += round16(total) + kMetaBytes;
-        g_stats.ns_device += now_ns() - t0;
-        return;
+    const bool reg = g_reg_min && !g_fake_devs && (C >= g_reg_min || total >= g_reg_min) &&
+                     !(g_zc_coop && C <= rle::kCoopDecMaxIn && U <= rle::kCoopDecUmax) && reg_likely();
+    const bool small = (C < kSegDecodeBytes && total <= kOneTripBytes) ||
+                       (g_zc_seg && g_zerocopy && C <= kZcMaxIn && total <= kZcMaxOut);
+    if (reg) {   // the registered path's buffers, grown before anything is registered
+        zc(c);
+        grow_dev(c->d_in, c->d_in_cap, round16(C));
+        grow_dev(c->d_out, c->d_out_cap, round16(total));
+        if (C >= kSegDecodeBytes) grow_dev(c->d_ws, c->d_ws_cap, rle_seg_workspace_bytes(1, C));
+        const LargeCall lc(c->s, data, C, r, total);
+        if (lc.registered()) return decompress_registered(c, lc, data, C, U, E, r);
+        g_stats.calls_reg_fallback++;
+        if (!small) return decompress_large(c, data, C, U, E, r);
+    } else if (!small) {
+        const LargeCall lc(c->s);
+        return decompress_large(c, data, C, U, E, r);
     }
+    // one wave walks it, or (g_zc_seg) the segmented kernels on the mapped buffer: the single-copy path
+    const uint64_t t0 = now_ns();
+    decompress_small(c, data, C, U, E, r);
+    g_stats.calls_decompress++;
+    g_stats.bytes_in += C;
+    g_stats.bytes_out += total;
+    g_stats.bytes_h2d += round16(C) + kMetaBytes;
+    g_stats.bytes_d2h += round16(total) + kMetaBytes;
+    g_stats.ns_device += now_ns() - t0;
+}
+
+namespace {
+void decompress_large(Ctx* c, const char* data, size_t C, size_t U, size_t E, char* r) {
+    const size_t total = U + E;
     grow_dev(c->d_in, c->d_in_cap, round16(C));
     grow_dev(c->d_out, c->d_out_cap, round16(total));
     const uint64_t t0 = now_ns();
@@ -1486,6 +1748,7 @@ static void decompress_impl(char* data, size_t C, size_t U, size_t E, char* r) {
     g_stats.ns_device += t2 - t1;
     g_stats.ns_stage_out += t3 - t2;
 }
+}  // namespace
 
 // src/rleCompression.c:47-62 — returns a malloc block of U+E bytes (decoded U, then E zeros); NULL
 // (errno = ENOMEM) when an allocation fails, as the reference's calloc can (:48).
@@ -1538,10 +1801,11 @@ static char* append_impl(char* content, size_t C, size_t U, const char* newConte
         g_stats.ns_device += now_ns() - t0;
         return out;
     }
+    const LargeCall lc(c->s);
     const size_t offA = round16(C) + 16;   // d_in: old stream | splice head (16 B) | new bytes
     const size_t inBytes = offA + A;
     // pinned staging only for the copies to_device stages (both, before either is queued)
-    grow_host(c->h_in, c->h_in_cap, std::max(staged(A) ? inBytes : 0, staged(C) ? C : 0));
+    grow_host(c->h_in, c->h_in_cap, std::max(staged(newContent, A) ? inBytes : 0, staged(content, C) ? C : 0));
     grow_dev(c->d_in, c->d_in_cap, round16(inBytes));
     grow_dev(c->d_mid, c->d_mid_cap, round16(U + A));
     const uint64_t t0 = now_ns();
@@ -1627,15 +1891,41 @@ struct NTotals {
 // RLEdecompressN of one file too large for the bounded staging: straight from / to caller memory
 // whatever RLE_MI355X_STAGING says (the pinned and pipe modes would grow this thread's staging to
 // the file's size, which g_stage_cap exists to prevent).
+// Bytes whose pages meet another call's registration (live_pages) go through the staging in
+// chunks of at most g_stage_cap instead, a synchronize per chunk.
 void decompress_n_alone(Ctx* c, const char* data, size_t C, size_t U, char* out, NTotals& t) {
+    const LargeCall lc(c->s);
     grow_dev(c->d_in, c->d_in_cap, round16(C));
     grow_dev(c->d_out, c->d_out_cap, round16(U));
+    const size_t ch = std::min(g_stage_cap, std::max(C, U));
+    const bool stage_in = live_pages(data, C), stage_out = U && live_pages(out, U);
+    if (stage_in) grow_host(c->h_in, c->h_in_cap, ch);
+    if (stage_out) grow_host(c->h_out, c->h_out_cap, ch);
     const uint64_t t0 = now_ns();
-    check(hipMemcpyAsync(c->d_in, data, C, hipMemcpyHostToDevice, c->s), "H2D");
+    if (!stage_in) {
+        check(hipMemcpyAsync(c->d_in, data, C, hipMemcpyHostToDevice, c->s), "H2D");
+    } else {
+        for (size_t off = 0; off < C; off += ch) {
+            const size_t len = std::min(ch, C - off);
+            memcpy(c->h_in, data + off, len);
+            check(hipMemcpyAsync(c->d_in + off, c->h_in, len, hipMemcpyHostToDevice, c->s), "H2D");
+            check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        }
+    }
     const uint64_t t1 = now_ns();
     queue_decode(c, c->d_in, C, c->d_out, U, U);
-    if (U) check(hipMemcpyAsync(out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
-    check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    if (!stage_out) {
+        if (U) check(hipMemcpyAsync(out, c->d_out, U, hipMemcpyDeviceToHost, c->s), "D2H");
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+    } else {
+        check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+        for (size_t off = 0; off < U; off += ch) {
+            const size_t len = std::min(ch, U - off);
+            check(hipMemcpyAsync(c->h_out, c->d_out + off, len, hipMemcpyDeviceToHost, c->s), "D2H");
+            check(hipStreamSynchronize(c->s), "hipStreamSynchronize");
+            memcpy(out + off, c->h_out, len);
+        }
+    }
     if ((uint32_t)c->h_meta[kMetaDec + 5] & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompressN");
     t.ns_in += t1 - t0;
     t.ns_dev += now_ns() - t1;
@@ -1804,12 +2094,16 @@ extern "C" int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset) {
     out->ns_stage_out = g_stats.ns_stage_out.load();
     out->calls_coalesced = g_stats.calls_coalesced.load();
     out->launches_coalesced = g_stats.launches_coalesced.load();
+    out->calls_registered = g_stats.calls_registered.load();
+    out->calls_reg_fallback = g_stats.calls_reg_fallback.load();
     if (reset) {
         g_stats.calls_compress = 0; g_stats.calls_decompress = 0; g_stats.calls_append = 0; g_stats.bytes_in = 0; g_stats.bytes_out = 0;
         g_stats.bytes_h2d = 0; g_stats.bytes_d2h = 0; g_stats.ns_stage_in = 0; g_stats.ns_device = 0;
         g_stats.ns_stage_out = 0;
         g_stats.calls_coalesced = 0;
         g_stats.launches_coalesced = 0;
+        g_stats.calls_registered = 0;
+        g_stats.calls_reg_fallback = 0;
     }
     return RLE_OK;
 }

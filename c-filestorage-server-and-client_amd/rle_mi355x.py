@@ -41,7 +41,7 @@ class DropinStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("calls_compress", "calls_decompress", "bytes_in", "bytes_out",
                                                "bytes_h2d", "bytes_d2h", "ns_stage_in", "ns_device",
                                                "ns_stage_out", "calls_append", "calls_coalesced",
-                                               "launches_coalesced")]
+                                               "launches_coalesced", "calls_registered", "calls_reg_fallback")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

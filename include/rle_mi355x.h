@@ -121,6 +121,9 @@ typedef struct {
     uint64_t calls_append;   /* RLEappend (include/rle_fileops.h); RLEdecompressN counts per file */
     uint64_t calls_coalesced, launches_coalesced;   /* zero-copy small calls and the combined launches
                                                        they ran in (concurrent callers share one) */
+    uint64_t calls_registered;     /* large calls run on the caller's registered memory (RLE_MI355X_REG_MIN) */
+    uint64_t calls_reg_fallback;   /* ... and those that took the staging instead (registration refused or
+                                      overlapping another call's) */
 } rle_dropin_stats_t;
 int rle_mi355x_dropin_stats(rle_dropin_stats_t* out, int reset);
 

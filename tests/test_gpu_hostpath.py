@@ -1,9 +1,11 @@
 """GPU tests of the drop-in's host path (BASELINE configs[4]).
 
-* Every staging mode of the large-call transfers (RLE_MI355X_STAGING = direct / pinned / pipe, read
-  at library init: a fresh process each) gives the oracle's bytes for RLEcompress / RLEdecompress
-  across the size thresholds (zero-copy small calls, pinned one-trip, segmented, >= 256 KiB
-  pipelined), for RLEappend and for RLEdecompressN with a file past the staging cap.
+* The registered large calls (the default past the zero-copy reach) and every staging mode a call
+  falls back to (RLE_MI355X_STAGING = direct / pinned / pipe, read at library init: a fresh process
+  each) give the oracle's bytes for RLEcompress / RLEdecompress across the size thresholds
+  (zero-copy small calls, pinned one-trip, segmented, >= 256 KiB), for RLEappend and for
+  RLEdecompressN with a file past the staging cap; registered calls from eight threads on buffers
+  that share pages, on one shared stream, on overlapping ranges and on read-only pages.
 * Concurrent small calls from many threads (the server's worker pool, src/server.c:520-524) stay
   bit-exact, on per-thread streams (the default) and combined into shared launches
   (RLE_MI355X_COALESCE=1): each thread's streams against the oracle, and the C call-rate tool's
@@ -53,13 +55,141 @@ print("ok", R.dropin_stats())
 VARIANTS_LIB = os.path.join(ROOT, "c-filestorage-server-and-client_amd", "build", "librle_mi355x_testhooks.so")
 
 
-@pytest.mark.parametrize("mode", ["direct", "pinned", "pipe"])
+@pytest.mark.parametrize("mode", ["registered", "direct", "pinned", "pipe"])
 def test_staging_modes_bit_exact(mode):
-    env = dict(os.environ, RLE_MI355X_STAGING=mode, RLE_MI355X_STAGE_CAP=str(1 << 20))
+    # "registered" is the default (large calls on the caller's registered memory); the staging modes
+    # are what a call falls back to, so they run with the registered path off
+    env = dict(os.environ, RLE_MI355X_STAGE_CAP=str(1 << 20))
+    if mode != "registered":
+        env.update(RLE_MI355X_STAGING=mode, RLE_MI355X_REG_MIN="0")
     if mode == "pipe":
         env["RLE_MI355X_LIB"] = VARIANTS_LIB
     r = subprocess.run([sys.executable, "-c", _STAGING_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+
+
+_REG_CODE = r'''
+import sys, ctypes, mmap, os, tempfile, threading
+sys.path[:0] = sys.argv[1:3]
+import numpy as np
+import rle_mi355x as R, rle_oracle as O
+L = ctypes.CDLL(R.lib()._name)
+sz = ctypes.c_size_t
+L.RLEcompress.restype = ctypes.c_void_p
+L.RLEcompress.argtypes = [ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+L.RLEdecompress.restype = ctypes.c_void_p
+L.RLEdecompress.argtypes = [ctypes.c_void_p, sz, sz, sz]
+free = R._libc.free
+
+def comp(addr, U):
+    c = sz(0)
+    p = L.RLEcompress(addr, U, ctypes.byref(c))
+    assert p
+    y = ctypes.string_at(p, c.value + 16)
+    free(p)
+    assert y[c.value:] == bytes(16)
+    return y[:c.value]
+
+def decomp(addr, C, U, E):
+    p = L.RLEdecompress(addr, C, U, E)
+    assert p
+    y = ctypes.string_at(p, U + E)
+    free(p)
+    return y
+
+R.dropin_stats(reset=True)
+# neighbouring slices of one buffer (their pages shared), odd sizes and offsets, kinds mixed
+sizes = [70001, 100003, 262145, 300007, 1048579, 777777, 2 << 20, 130001]
+offs = [16 + sum(sizes[:i]) + 3 * i for i in range(len(sizes))]
+big = np.zeros(offs[-1] + sizes[-1] + 64, dtype=np.uint8)
+xs = [O.gen(i % 4, 300 + i, U) for i, U in enumerate(sizes)]
+for o, x in zip(offs, xs):
+    big[o:o + len(x)] = np.frombuffer(x, dtype=np.uint8)
+ys = [O.encode(x) for x in xs]
+yoffs = [8 + sum(len(y) for y in ys[:i]) + 5 * i for i in range(len(ys))]
+ybig = np.zeros(yoffs[-1] + len(ys[-1]) + 64, dtype=np.uint8)
+for o, y in zip(yoffs, ys):
+    ybig[o:o + len(y)] = np.frombuffer(y, dtype=np.uint8)
+base, ybase = big.ctypes.data, ybig.ctypes.data
+errors = []
+# alone: registered
+assert comp(base + offs[4], sizes[4]) == ys[4]
+assert decomp(ybase + yoffs[4], len(ys[4]), sizes[4], 100) == xs[4] + bytes(100)
+assert R.dropin_stats()["calls_registered"] == 2, R.dropin_stats()
+
+def work(t):
+    try:
+        for rep in range(3):
+            for k in range(len(sizes)):
+                i = (k + t) % len(sizes)
+                if comp(base + offs[i], sizes[i]) != ys[i]:
+                    errors.append(("c", t, i))
+                E = 0 if (t + rep) % 2 else 4097
+                if decomp(ybase + yoffs[i], len(ys[i]), sizes[i], E) != xs[i] + bytes(E):
+                    errors.append(("d", t, i))
+                # every thread also reads the same stored stream (one shared registration)
+                if decomp(ybase + yoffs[6], len(ys[6]), sizes[6], 0) != xs[6]:
+                    errors.append(("s", t))
+    except Exception as e:   # noqa: BLE001
+        errors.append(repr(e))
+
+# beside them, the readN and append paths on the same stored stream (a file past the staging cap
+# set for this process: its bytes go straight from / to caller memory, or through the staging in
+# chunks while another call holds a registration)
+def other(t):
+    try:
+        for rep in range(4):
+            y6 = ctypes.string_at(ybase + yoffs[6], len(ys[6]))
+            if R.decompress_n([y6, ys[1]], [sizes[6], sizes[1]]) != [xs[6], xs[1]]:
+                errors.append(("n", t))
+            if R.append(y6, sizes[6], xs[3]) != O.encode(xs[6] + xs[3]):
+                errors.append(("a", t))
+    except Exception as e:   # noqa: BLE001
+        errors.append(repr(e))
+
+th = [threading.Thread(target=work, args=(t,)) for t in range(8)] + [threading.Thread(target=other, args=(9,))]
+for t in th: t.start()
+for t in th: t.join()
+assert not errors, errors[:10]
+# overlapping ranges of one buffer from two threads
+x2 = O.gen(2, 99, 3 << 20)
+b2 = np.frombuffer(x2, dtype=np.uint8).copy()
+refs = {(0, 2 << 20): O.encode(x2[:2 << 20]), (1 << 20, 2 << 20): O.encode(x2[1 << 20:3 << 20])}
+def ov(o):
+    for _ in range(6):
+        if comp(b2.ctypes.data + o, 2 << 20) != refs[(o, 2 << 20)]:
+            errors.append(("ov", o))
+th = [threading.Thread(target=ov, args=(o,)) for o in (0, 1 << 20)]
+for t in th: t.start()
+for t in th: t.join()
+assert not errors, errors[:10]
+# read-only pages: a file mapped read-only
+x3 = O.gen(3, 5, 1500000)
+with tempfile.NamedTemporaryFile(delete=False) as f:
+    f.write(x3)
+with open(f.name, "rb") as fh:
+    mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+    a = np.frombuffer(mm, dtype=np.uint8)
+    assert comp(a.ctypes.data, len(x3)) == O.encode(x3)
+    del a
+    mm.close()
+os.unlink(f.name)
+st = R.dropin_stats()
+assert st["calls_registered"] > 0, st
+print("ok", st)
+'''
+
+
+def test_registered_large_calls_concurrent_bit_exact():
+    """Large calls on the caller's registered memory (the default past 256 KiB, when a call is the
+    only large call in flight; csrc/rle_dropin.cpp LargeCall): alone; eight threads on neighbouring
+    slices of one buffer, whose pages they share, and on one stored stream that all of them read
+    while a ninth runs readN and append on it (past a 1 MiB staging cap); two threads on overlapping
+    ranges; a read-only mapped file; all bit-exact against the oracle."""
+    r = subprocess.run([sys.executable, "-c", _REG_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
+                        os.path.join(ROOT, "oracle")], env=dict(os.environ, RLE_MI355X_STAGE_CAP=str(1 << 20)),
+                       capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
 
 

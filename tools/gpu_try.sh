@@ -7,7 +7,7 @@ for i in $(seq 1 15); do
   /usr/local/graft/bin/gpurun --timeout $TO -- "$CMD" > $LOG 2>&1
   rc=$?
   [ $rc -ne 3 ] && exit $rc
-  grep -q "no free box\|backing off\|busy" $LOG || exit $rc
+  grep -q "no free box\|backing off\|busy\|while being prepared" $LOG || exit $rc
   sleep 150
 done
 exit 3

@@ -58,12 +58,15 @@ def one(kind, U, seconds):
 
 
 def threads(T, U, seconds):
+    """T threads, each round-tripping its own U random bytes (the server's requests each have their
+    own buffers, src/server.c:150-151)."""
     L = R.lib()
-    x = gen("random", U, 7)
+    xs = [gen("random", U, 7 + i) for i in range(T)]
     counts = [0] * T
     stop = time.perf_counter() + seconds
 
     def work(i):
+        x = xs[i]
         c = ctypes.c_size_t(0)
         while time.perf_counter() < stop:
             p = L.RLEcompress(x, U, ctypes.byref(c))
@@ -172,11 +175,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--only", choices=["single", "threads", "fileops"], default=None)
+    ap.add_argument("--sizes", default="4096,65536,1048576,4194304", help="single-call sizes, bytes")
     a = ap.parse_args()
     R.dropin_stats(reset=True)
     res = {"single": [], "threads": []}
     if a.only in (None, "single"):
-        for U in (4096, 65536, 1 << 20, 4 << 20):
+        for U in (int(v) for v in a.sizes.split(",")):
             for kind in ("random", "zero", "runs"):
                 res["single"].append(one(kind, U, a.seconds))
     if a.only in (None, "fileops"):
