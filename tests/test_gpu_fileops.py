@@ -71,6 +71,24 @@ def test_append_large_and_segmented_sizes():
         assert R.append(y, len(old), new) == O.encode(old + new), (len(old), len(new))
 
 
+def test_append_zero_copy_sizes():
+    """The zero-copy append (csrc/rle_dropin.cpp append_small_zc): old streams the one-wave or the
+    cooperative decode takes from the mapped buffer (up to 80 tiles decoding to 64 KiB), new bytes
+    up to the cooperative encode's 64 KiB, at and around their edges; a stream that is not encoder
+    output in that range falls back to the whole re-encode."""
+    cases = []
+    for kind, U, A in [(1, 4096, 4096), (2, 32000, 100), (1, 33000, 1), (2, 65536, 4096), (3, 65536, 65520),
+                       (1, 53000, 60000), (0, 65536, 0), (1, 65536, 65521), (2, 40000, 70000)]:
+        cases.append((O.gen(kind, U + A, U), O.gen((kind + 1) % 4, U ^ A, A)))
+    for old, new in cases:
+        y = O.encode(old)
+        assert R.append(y, len(old), new) == O.encode(old + new), (len(old), len(y), len(new))
+    # hand-made: a long literal stream whose last token is not the encoder's
+    y = O.encode(O.gen(1, 77, 40000))
+    bad = y[:-1] + (b"5" if y[-1:] != b"5" else b"6")
+    assert R.append(bad, 40000, b"zz") == ref_append(bad, 40000, b"zz")
+
+
 def test_append_empty_and_not_encoder_streams():
     assert R.append(b"", 0, b"") == b""
     assert R.append(b"", 0, b"aaab") == b"aa3b"
