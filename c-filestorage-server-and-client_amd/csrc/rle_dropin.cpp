@@ -2053,6 +2053,61 @@ void decompress_n_chunk(Ctx* c, size_t* idx, size_t m, char* const* data, const 
     t.d2h += outTot;
 }
 
+// A chunk of small files through this thread's mapped buffer (round 6; g_zerocopy): the streams
+// copied into its input region, one launch over them, the decoded files written into its output
+// region, the per-file status words polled (each stored behind a system-scope release of its file),
+// no copy commands.  Files a one-wave or cooperative decode takes (zc_n_fits), at most kZcNFiles
+// (the metadata fits the words region) and the mapped regions' bytes per chunk.
+// (Files up to 16 KiB: a 64 KiB file's one-wave decode writing over PCIe took 200 µs per chunk of
+// five, r6aa: 64 x 64 KiB zero 2266 µs against 456 staged.)
+constexpr size_t kZcNFiles = 96;   // 36 bytes of launch words each, inside the 4 KiB words region
+constexpr size_t kZcNMaxU = 16384;
+bool zc_n_fits(size_t C, size_t U) {
+    return g_zerocopy && C < kSegDecodeBytes && U <= kZcNMaxU;
+}
+void decompress_n_chunk_zc(Ctx* c, const size_t* idx, size_t m, char* const* data, const size_t* compressedSize,
+                           const size_t* uncompressedSize, char* const* out, NTotals& t) {
+    uint8_t* h = zc(c);
+    uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
+    uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
+    uint32_t* hst = reinterpret_cast<uint32_t*>(hw + 4 * m);
+    const uint64_t t0 = now_ns();
+    size_t io = 0, oo = 0, maxC = 0, maxU = 0;
+    for (size_t k = 0; k < m; ++k) {
+        const size_t i = idx[k], C = compressedSize[i], U = uncompressedSize[i];
+        hw[k] = kZcIn + io; hw[m + k] = C; hw[2 * m + k] = kZcOut + oo; hw[3 * m + k] = U;
+        hst[k] = kPending;
+        memcpy(h + kZcIn + io, data[i], C);
+        io += round16(C);
+        oo += round16(U);
+        maxC = std::max(maxC, C);
+        maxU = std::max(maxU, U);
+    }
+    const uint64_t t1 = now_ns();
+    if (rle_decode_batch_device_sized_flags(c->d_zc, dw, dw + m, c->d_zc, dw + 2 * m, dw + 3 * m, nullptr,
+                                            reinterpret_cast<uint32_t*>(dw + 4 * m), (uint32_t)m, maxC, maxU,
+                                            RLE_LAUNCH_STATUS_FLAG, c->s) != RLE_OK)
+        die("decode launch", hipGetLastError());
+    // every file's status (the launch's last stores are in no particular order); zc_wait's bounds
+    // and periodic synchronize, counted once per launch
+    const uint32_t polled = c->polled;
+    for (size_t k = 0; k < m; ++k) {
+        c->polled = polled;
+        (void)zc_wait(c, reinterpret_cast<const uint64_t*>(hst + k));
+    }
+    const uint64_t t2 = now_ns();
+    for (size_t k = 0; k < m; ++k) {
+        const size_t i = idx[k], U = uncompressedSize[i];
+        if (U) memcpy(out[i], h + hw[2 * m + k], U);
+        if (hst[k] & RLE_STATUS_OVERFLOW) warn_overflow("RLEdecompressN");
+    }
+    t.ns_in += t1 - t0;
+    t.ns_dev += t2 - t1;
+    t.ns_out += now_ns() - t2;
+    t.h2d += io;
+    t.d2h += oo;
+}
+
 int decompress_n_impl(size_t n, char* const* data, const size_t* compressedSize, const size_t* uncompressedSize,
                       char* const* out) {
     std::vector<size_t> idx;
@@ -2073,18 +2128,26 @@ int decompress_n_impl(size_t n, char* const* data, const size_t* compressedSize,
     if (idx.empty()) return 0;
     Ctx* c = ctx();
     NTotals t;
-    // files in batch order: chunks of consecutive files that fit the staging together, files too
-    // large for it alone
+    // files in batch order: chunks of consecutive small files through the mapped buffer (zc_n_fits),
+    // chunks of consecutive files that fit the staging together, files too large for it alone
     size_t k0 = 0, inTot = 0, outTot = 0;
+    bool zcChunk = false;
     for (size_t k = 0; k <= idx.size(); ++k) {
         const bool end = k == idx.size();
         const size_t Ci = end ? 0 : round16(compressedSize[idx[k]]), Ui = end ? 0 : round16(uncompressedSize[idx[k]]);
+        const bool zcFile = !end && zc_n_fits(compressedSize[idx[k]], uncompressedSize[idx[k]]);
         const bool alone = !end && (Ci > g_stage_cap || Ui > g_stage_cap);
-        if (end || alone || inTot + Ci > g_stage_cap || outTot + Ui > g_stage_cap) {
-            if (k > k0) decompress_n_chunk(c, idx.data() + k0, k - k0, data, compressedSize, uncompressedSize, out, t);
+        const bool full = zcChunk ? (inTot + Ci > kZcWords || outTot + Ui > kZcMaxOut || k - k0 >= kZcNFiles)
+                                  : (inTot + Ci > g_stage_cap || outTot + Ui > g_stage_cap);
+        if (end || alone || full || (k > k0 && zcFile != zcChunk)) {
+            if (k > k0 && zcChunk)
+                decompress_n_chunk_zc(c, idx.data() + k0, k - k0, data, compressedSize, uncompressedSize, out, t);
+            else if (k > k0)
+                decompress_n_chunk(c, idx.data() + k0, k - k0, data, compressedSize, uncompressedSize, out, t);
             k0 = k;
             inTot = outTot = 0;
         }
+        zcChunk = zcFile;
         if (alone) {
             const size_t i = idx[k];
             decompress_n_alone(c, data[i], compressedSize[i], uncompressedSize[i], out[i], t);
