@@ -101,6 +101,16 @@ def test_append_empty_and_not_encoder_streams():
         assert R.append(content, U, new) == ref_append(content, U, new), (content, U, new)
 
 
+def test_decompress_n_zero_copy_chunks():
+    """Small files go through the mapped buffer in chunks (csrc/rle_dropin.cpp decompress_n_chunk_zc):
+    more files than one chunk's launch words (96), inputs past the 256 KiB input region, 16 KiB
+    files at the size limit, then one past it, and small files again after it."""
+    xs = [O.gen(k % 4, k, 100 + (k * 37) % 4000) for k in range(250)]
+    xs += [O.gen(1, 1000 + k, 16384) for k in range(40)] + [O.gen(2, 7, 16385)] + [O.gen(3, 8, 500)] * 5
+    ys = [O.encode(x) for x in xs]
+    assert R.decompress_n(ys, [len(x) for x in xs]) == xs
+
+
 def test_decompress_n_matches_per_file_decodes():
     rng = np.random.default_rng(7)
     xs = [O.gen(i % 5, i, int(rng.integers(0, 20000))) for i in range(300)]
