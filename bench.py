@@ -334,10 +334,11 @@ def load_pmc(workload):
 
 
 # ------------------------------------------------------------------------------------ the exchange
-# Why "inline" is the default exchange mode: it is the only mode measured faster.
-XMODE_REASON = ("inline: measured 29.4 us per configs[1] step against 35.0 (async) and 45.0 (graph) in the "
-                "one-rank RCCL rehearsal (DESIGN.md s7, r3b); async's overlap of the gather is unmeasured at "
-                "N > 1 (one GPU per box), so it stays opt-in (RLE_BENCH_XMODE=async)")
+# The exchange mode: "auto" times inline and async on the job's own ranks and keeps the faster.
+XMODE_REASON = ("auto: inline and async timed on the job's own ranks before the timed region, the faster kept "
+                "(auto_us_per_step); one-rank RCCL rehearsal (DESIGN.md s7, r3b): inline 29.4 us per configs[1] "
+                "step against 35.0 (async) and 45.0 (graph); async's overlap of the gather is unmeasured at N > 1 "
+                "on this pool's one-GPU boxes")
 class Exchange:
     """The N > 1 exchange step of one rank: after a step's encode, its compressed
     sizes are all-gathered and scanned into global stream offsets.  Modes (RLE_BENCH_XMODE):
@@ -524,10 +525,10 @@ def run_rank(args):
         stream = torch.cuda.current_stream()
         B = Batch(wl, rank, world, dev)
 
-    xmode = os.environ.get("RLE_BENCH_XMODE", "inline")
-    if xmode not in ("async", "inline", "graph"):
-        raise SystemExit(f"RLE_BENCH_XMODE={xmode}: async, inline or graph")
-    xch = Exchange(B, world, rank, dev, dry, xmode) if multi else None
+    xmode = os.environ.get("RLE_BENCH_XMODE", "auto")
+    if xmode not in ("auto", "async", "inline", "graph"):
+        raise SystemExit(f"RLE_BENCH_XMODE={xmode}: auto, async, inline or graph")
+    xch = Exchange(B, world, rank, dev, dry, "inline" if xmode == "auto" else xmode) if multi else None
     if xch is not None and xch.mode == "torch" and not dry and rank == 0:
         print(f"native exchange unavailable ({xch.error}); torch calls", file=sys.stderr)
     loop = Loop(B, xch, stream, dry)
@@ -569,6 +570,30 @@ def run_rank(args):
             loop.plain = False
             loop.graphs.clear()
     loop.steps(max(1, args.warmup))
+    # RLE_BENCH_XMODE=auto (the default): the exchange mode is chosen on this job's own ranks, before
+    # the timed region -- K steps inline and K steps async, each timed between barriers, the max over
+    # ranks, the faster mode kept (every rank takes the same numbers).  At one rank inline measured
+    # faster (XMODE_REASON); at N > 1 the all-gather's latency over xGMI can exceed a step, which
+    # async overlaps with the decode and the next encode.  Its result is verified as inline's was.
+    auto = None
+    if xch is not None and xmode == "auto" and xch.mode == "inline" and not dry:
+        auto = {}
+        for mode in ("inline", "async"):
+            xch.mode = mode
+            loop.steps(max(1, args.warmup))
+            sync(dry)
+            dist.barrier()
+            ta = time.perf_counter()
+            loop.steps(args.steps)
+            sync(dry)
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - ta], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            auto[mode] = round(float(t.item()) / args.steps * 1e6, 2)
+        xch.mode = min(auto, key=auto.get)
+        loop.one_step(0)
+        offsets_ok = offsets_ok and xch.verify(stream)
+        loop.steps(max(1, args.warmup))
 
     if multi:
         dist.barrier()
@@ -691,7 +716,8 @@ def run_rank(args):
                "cpu_baseline": cpu, "north_star_dec64k": north, "concurrent_streams": conc}
         if xch is not None:
             out["exchange"] = {"mode": xch.mode, "offsets_match_process_group": offsets_ok, "graph_captured": graph_ok,
-                               "error": str(xch.error) if xch.error else None, "default_mode_reason": XMODE_REASON}
+                               "error": str(xch.error) if xch.error else None, "default_mode_reason": XMODE_REASON,
+                               "auto_us_per_step": auto}
         if dry:
             out["dry_run"] = True
         print(json.dumps(out), flush=True)

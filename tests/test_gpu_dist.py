@@ -116,12 +116,12 @@ def test_exchange_captured_in_graph_one_rank():
         R.dist_finalize()
 
 
-@pytest.mark.parametrize("xmode", ["async", "inline", "graph"])
+@pytest.mark.parametrize("xmode", ["async", "inline", "graph", "auto"])
 def test_bench_exchange_path_one_rank(xmode):
     """bench.py's N > 1 rank loop rehearsed on one GPU (RLE_BENCH_FORCE_EXCHANGE=1): a one-rank
     process group over RCCL, the native exchange in each mode (side stream, codec stream, captured
-    with the timed loop in one HIP graph), the offsets checked against the process-group path, and
-    the round trip verified."""
+    with the timed loop in one HIP graph, and the default: inline and async timed, the faster
+    kept), the offsets checked against the process-group path, and the round trip verified."""
     import json
     import os
     import subprocess
@@ -135,7 +135,11 @@ def test_bench_exchange_path_one_rank(xmode):
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["verified_bit_exact_roundtrip"] is True
-    assert out["exchange"]["mode"] == xmode, out["exchange"]
+    if xmode == "auto":
+        t = out["exchange"]["auto_us_per_step"]
+        assert set(t) == {"inline", "async"} and out["exchange"]["mode"] == min(t, key=t.get), out["exchange"]
+    else:
+        assert out["exchange"]["mode"] == xmode, out["exchange"]
     assert out["exchange"]["graph_captured"] is (True if xmode == "graph" else None)
     assert out["exchange"]["offsets_match_process_group"] is True
 
