@@ -2060,7 +2060,7 @@ void decompress_n_chunk(Ctx* c, size_t* idx, size_t m, char* const* data, const 
 // (the metadata fits the words region) and the mapped regions' bytes per chunk.
 // (Files up to 16 KiB: a 64 KiB file's one-wave decode writing over PCIe took 200 µs per chunk of
 // five, r6aa: 64 x 64 KiB zero 2266 µs against 456 staged.)
-constexpr size_t kZcNFiles = 96;   // 36 bytes of launch words each, inside the 4 KiB words region
+constexpr size_t kZcNFiles = 56;   // 36 bytes of launch words each, below kZcWords + 2048 (kZcMail)
 constexpr size_t kZcNMaxU = 16384;
 bool zc_n_fits(size_t C, size_t U) {
     return g_zerocopy && C < kSegDecodeBytes && U <= kZcNMaxU;

@@ -103,7 +103,7 @@ def test_append_empty_and_not_encoder_streams():
 
 def test_decompress_n_zero_copy_chunks():
     """Small files go through the mapped buffer in chunks (csrc/rle_dropin.cpp decompress_n_chunk_zc):
-    more files than one chunk's launch words (96), inputs past the 256 KiB input region, 16 KiB
+    more files than one chunk's launch words (56), inputs past the 256 KiB input region, 16 KiB
     files at the size limit, then one past it, and small files again after it."""
     xs = [O.gen(k % 4, k, 100 + (k * 37) % 4000) for k in range(250)]
     xs += [O.gen(1, 1000 + k, 16384) for k in range(40)] + [O.gen(2, 7, 16385)] + [O.gen(3, 8, 500)] * 5
