@@ -193,6 +193,26 @@ def test_registered_large_calls_concurrent_bit_exact():
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
 
 
+def test_registered_calls_on_streams_the_encoder_never_writes():
+    """Registered decompress (past 256 KiB) of streams that are not encoder output, with an extra
+    region: the exact serial decode may write into the E region, which then travels too
+    (decompress_registered); streams that decode short of U, past U, and exactly to it."""
+    rng = __import__("random").Random(5)
+    cases = []
+    for C in (300001, 700000, 1 << 20):
+        s = rng.randbytes(C)   # random bytes read as a stream
+        for U, E in ((C // 2, 4096), (C, 100), (2 * C, 333), (C + 7, 0)):
+            cases.append((s, U, E))
+    # an encoder stream with a digit run rewritten (decodes past U), and a valid one cut short
+    y = O.encode(O.gen(3, 11, 900000))
+    cases.append((y[:len(y) // 2] + b"779" * 1000 + y[len(y) // 2:], 900000, 5000))
+    cases.append((y, 800000, 12345))
+    for s, U, E in cases:
+        got = R.decompress(s, U, E)
+        ref, _ = O.decode(s, U, U + E)
+        assert got == ref, (len(s), U, E)
+
+
 _COALESCE_CODE = r'''
 import sys, threading
 sys.path[:0] = sys.argv[1:3]
