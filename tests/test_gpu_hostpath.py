@@ -188,7 +188,9 @@ def test_registered_large_calls_concurrent_bit_exact():
     while a ninth runs readN and append on it (past a 1 MiB staging cap); two threads on overlapping
     ranges; a read-only mapped file; all bit-exact against the oracle."""
     r = subprocess.run([sys.executable, "-c", _REG_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
-                        os.path.join(ROOT, "oracle")], env=dict(os.environ, RLE_MI355X_STAGE_CAP=str(1 << 20)),
+                        os.path.join(ROOT, "oracle")],
+                       env=dict(os.environ, RLE_MI355X_STAGE_CAP=str(1 << 20), RLE_MI355X_REG_MIN=str((256 << 10) + 1),
+                                RLE_MI355X_REG_QUIET_US="2000"),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
 
@@ -253,8 +255,9 @@ def test_concurrent_small_calls_coalesced_bit_exact():
     against the oracle; the library counts every small call as combined."""
     # (no background start-up: its warm-up calls would be combined too, after the counters' reset)
     # (and the one-wave zero-copy range only: the count below is of calls under 48 / 32 KiB)
+    # (coalescing combines zero-copy calls: RLE_MI355X_SMALL from the caller's environment is reset)
     env = dict(os.environ, RLE_MI355X_COALESCE="1", RLE_MI355X_LIB=VARIANTS_LIB, RLE_MI355X_PREINIT="0",
-               RLE_MI355X_ZC_SEG="0")
+               RLE_MI355X_ZC_SEG="0", RLE_MI355X_SMALL="zerocopy")
     r = subprocess.run([sys.executable, "-c", _COALESCE_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
                         os.path.join(ROOT, "oracle")], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
