@@ -267,7 +267,9 @@ public:
         const uint64_t t = now_ns();
         const int n = ++g_large_calls;
         if (n > 1) g_last_overlap_ns = t;
-        if (in && n == 1 && t - g_last_overlap_ns > g_reg_quiet_ns && (d_in = reg_one(in, n_in, true))) {
+        // (the input and the result block must not share a page: the input is registered read-only)
+        const bool apart = !in || !out || page_hi(in, n_in) <= page_lo(out) || page_hi(out, n_out) <= page_lo(in);
+        if (in && apart && n == 1 && t - g_last_overlap_ns > g_reg_quiet_ns && (d_in = reg_one(in, n_in, true))) {
             if ((d_out = reg_one(out, n_out, false))) {
                 in_ = in;
                 out_ = out;
