@@ -248,7 +248,7 @@ uint8_t* reg_one(const void* p, size_t n, bool read_only) {
     return static_cast<uint8_t*>(d);
 }
 void unreg_all(const void* in, const void* out) {   // (the registered call's two, in that order)
-    if (out) (void)hipHostUnregister(const_cast<void*>(out));
+    (void)hipHostUnregister(const_cast<void*>(out));
     (void)hipHostUnregister(const_cast<void*>(in));
     (void)hipGetLastError();
     g_live_regs = 0;
@@ -267,28 +267,10 @@ public:
         const uint64_t t = now_ns();
         const int n = ++g_large_calls;
         if (n > 1) g_last_overlap_ns = t;
-        if (!in || n != 1 || t - g_last_overlap_ns <= g_reg_quiet_ns) return;
-        // The input and the result block side by side on the heap share a page: one registration
-        // covers both (read-write), so that no page is registered twice with different rights.
-        const bool apart = page_hi(in, n_in) <= page_lo(out) || page_hi(out, n_out) <= page_lo(in);
-        if (!apart) {
-            const uintptr_t a = std::min((uintptr_t)in, (uintptr_t)out);
-            const uintptr_t b = std::max((uintptr_t)in + n_in, (uintptr_t)out + n_out);
-            uint8_t* d = reg_one(reinterpret_cast<const void*>(a), b - a, false);
-            if (!d) return;
-            d_in = d + ((uintptr_t)in - a);
-            d_out = d + ((uintptr_t)out - a);
-            if ((uintptr_t)d_out & 15u) {   // (the copy kernel's alignment: as reg_one checks)
-                (void)hipHostUnregister(reinterpret_cast<void*>(a));
-                (void)hipGetLastError();
-                g_live_regs = 0;
-                d_in = d_out = nullptr;
-                return;
-            }
-            in_ = reinterpret_cast<const void*>(a);
-            return;
-        }
-        if ((d_in = reg_one(in, n_in, true))) {
+        if (in && n == 1 && t - g_last_overlap_ns > g_reg_quiet_ns && (d_in = reg_one(in, n_in, true))) {
+            // (the input and the result block may share a page when malloc put them side by side:
+            // a read-only and a read-write registration of one page measured correct,
+            // tools/probes/reg_shared_page_probe.hip, r6ao)
             if ((d_out = reg_one(out, n_out, false))) {
                 in_ = in;
                 out_ = out;
@@ -303,7 +285,7 @@ public:
     ~LargeCall() {
         if (registered()) (void)hipStreamSynchronize(s_);
         std::lock_guard<std::mutex> g(g_reg_mu);
-        if (registered()) unreg_all(in_, out_);   // (out_ null: one registration of both)
+        if (registered()) unreg_all(in_, out_);
         --g_large_calls;
     }
     LargeCall(const LargeCall&) = delete;
