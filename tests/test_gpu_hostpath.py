@@ -345,8 +345,11 @@ for k, U in enumerate([65537, 80640, 80641, 98304, 131072, 200000, 262143, 26214
     if R.compress(x) != y:
         errors.append(("enc-big", k, U))
     E = 393216 - U if k % 2 == 0 and U < 393216 else 0   # the output region's reach, exactly
-    if R.decompress(y, U, E) != x + bytes(E):
-        errors.append(("dec-big", k, U, E))
+    got = R.decompress(y, U, E)
+    if got != x + bytes(E):   # (where and how: the first differing byte, the path's counters)
+        want = x + bytes(E)
+        i = next(j for j in range(len(want)) if j >= len(got) or got[j] != want[j])
+        errors.append(("dec-big", k, U, E, len(y), i, got[i:i + 8].hex(), want[i:i + 8].hex(), R.dropin_stats()))
 
 def work(t):
     try:
