@@ -18,7 +18,9 @@ def _ref_offsets(gathered, world, n):
 
 
 @pytest.mark.parametrize("world,n", [(1, 1), (2, 7), (3, 1000), (8, 4096), (8, 131072), (1, 1 << 20),
-                                     (5, 300000), (16, 65537), (17, 1000)])
+                                     (5, 300000), (16, 65537), (17, 1000),
+                                     # just past the one-workgroup form (n <= 512), and around 8192
+                                     (1, 513), (8, 1025), (2, 8191), (16, 8192), (3, 8193)])
 def test_offsets_kernel_global_order(world, n):
     rng = np.random.default_rng(world * 1000 + n)
     g = rng.integers(0, 70000, size=world * n, dtype=np.int64)
