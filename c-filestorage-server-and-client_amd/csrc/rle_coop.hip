@@ -535,6 +535,24 @@ __global__ __launch_bounds__(kWave* kW) void dec_coop_kernel(const uint8_t* __re
     dec_coop_body<kW, kUmax, false, kR>(in + in_off[b], out + out_off[b], in_len[b], out_len[b], capp[b], status, b, wt);
 }
 
+// One buffer whose sizes the host knows (the drop-in's zero-copy calls, round 6): the same bodies
+// with the sizes and addresses as kernel arguments, so that the first tiles' loads do not wait for a
+// read of the launch words over PCIe.
+template <u32 kW, u32 kR = 1>
+__global__ __launch_bounds__(kWave* kW) void enc_coop_one_kernel(const uint8_t* __restrict__ src,
+                                                                 uint8_t* __restrict__ dst, uint64_t U,
+                                                                 uint64_t* __restrict__ out_len,
+                                                                 uint32_t* __restrict__ status, uint32_t wt) {
+    enc_coop_body<kW, false, kR>(src, dst, U, out_len, status, 0u, wt);
+}
+template <u32 kW, u32 kUmax, u32 kR = 1>
+__global__ __launch_bounds__(kWave* kW) void dec_coop_one_kernel(const uint8_t* __restrict__ src,
+                                                                 uint8_t* __restrict__ dst, uint64_t C, uint64_t U,
+                                                                 uint64_t cap, uint32_t* __restrict__ status,
+                                                                 uint32_t wt) {
+    dec_coop_body<kW, kUmax, false, kR>(src, dst, C, U, cap, status, 0u, wt);
+}
+
 #if RLE_VARIANTS   // the resident service is built into the test library only (round 5)
 // ================================================================ resident small-call service
 // (rle_service.h): one workgroup per drop-in thread context.  Wave 0 polls the context's mailbox
@@ -737,6 +755,89 @@ extern "C" int rle_decode_coop_launch(const void* d_in, const uint64_t* d_in_off
     }
 #undef RLE_DEC_COOP
 #undef RLE_DEC_COOP_R
+    return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
+}
+
+// One buffer with its sizes by value (csrc/rle_dropin.cpp's zero-copy calls): the same
+// instantiations as the batched launches above choose for these sizes.  1 launched, 0 the buffer
+// does not qualify (the caller launches the one-wave kernels), < 0 a launch error.
+namespace {
+bool coop_one_on() {   // (A/B) RLE_MI355X_COOP_ONE=0: the batched entry points for single calls too
+    static const bool on = [] {
+        const char* e = getenv("RLE_MI355X_COOP_ONE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+}  // namespace
+extern "C" int rle_encode_coop_one(const void* src, void* dst, uint64_t U, uint64_t* d_out_len, uint32_t* d_status,
+                                   uint32_t flags, void* stream) {
+    if (!coop_one_on()) return 0;
+    if (U > rle::kEncStep * rle::kCoopMaxWaves * rle::kCoopEncRounds || U <= rle::kEncStep) return 0;
+    const uint32_t tiles = (uint32_t)((U + rle::kEncStep - 1) / rle::kEncStep);
+    if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t wt = coop_store_policy(1u) | flags;
+#define RLE_ENC_ONE(W, R)                                                                                          \
+    do {                                                                                                           \
+        if (!coop_admits<rle::enc_coop_kernel<W, R>>(64 * W, 1u)) return 0;                                       \
+        hipLaunchKernelGGL((rle::enc_coop_one_kernel<W, R>), dim3(1), dim3(64 * W), 0, s, (const uint8_t*)src,     \
+                           (uint8_t*)dst, U, d_out_len, d_status, wt);                                             \
+    } while (0)
+    if (tiles <= 2) RLE_ENC_ONE(2, 1);
+    else if (tiles <= 3) RLE_ENC_ONE(3, 1);
+    else if (tiles <= 4) RLE_ENC_ONE(4, 1);
+    else if (tiles <= 6) RLE_ENC_ONE(6, 1);
+    else if (tiles <= 8) RLE_ENC_ONE(8, 1);
+    else if (tiles <= 12) RLE_ENC_ONE(12, 1);
+    else if (tiles <= 16) RLE_ENC_ONE(16, 1);
+    else if (tiles <= 32) RLE_ENC_ONE(16, 2);
+    else RLE_ENC_ONE(16, 4);
+#undef RLE_ENC_ONE
+    return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
+}
+extern "C" int rle_decode_coop_one(const void* src, void* dst, uint64_t C, uint64_t U, uint64_t cap, uint32_t* d_status,
+                                   uint32_t flags, void* stream) {
+    if (!coop_one_on()) return 0;
+    if (C > (uint64_t)rle::kTileStep * rle::kCoopMaxWaves * rle::kCoopDecRounds || C <= rle::kTileStep ||
+        U > rle::kCoopDecUmax)
+        return 0;
+    const uint32_t tiles = (uint32_t)((C + rle::kTileStep - 1) / rle::kTileStep);
+    if (g_coop_mode.load(std::memory_order_relaxed) == 0) return 0;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t wt = coop_store_policy(1u) | flags;
+#define RLE_DEC_ONE_R(W, UM, R)                                                                                   \
+    do {                                                                                                          \
+        if (!coop_admits<rle::dec_coop_kernel<W, UM, R>>(64 * W, 1u)) return 0;                                   \
+        hipLaunchKernelGGL((rle::dec_coop_one_kernel<W, UM, R>), dim3(1), dim3(64 * W), 0, s, (const uint8_t*)src, \
+                           (uint8_t*)dst, C, U, cap, d_status, wt);                                               \
+    } while (0)
+#define RLE_DEC_ONE(W, UM) RLE_DEC_ONE_R(W, UM, 1)
+    if (U > 32768u) {   // 32-64 KiB: rounds of 16 tiles
+        RLE_DEC_ONE_R(16, 65536, 5);
+    } else if (U > 16384u) {
+        if (tiles <= 4) RLE_DEC_ONE(4, 32768);
+        else if (tiles <= 8) RLE_DEC_ONE(8, 32768);
+        else if (tiles <= 16) RLE_DEC_ONE(16, 32768);
+        else if (tiles <= 48) RLE_DEC_ONE_R(16, 32768, 3);
+        else RLE_DEC_ONE_R(16, 32768, 4);
+    } else if (tiles > 16) {
+        RLE_DEC_ONE_R(16, 16384, 2);
+    } else if (U <= 4096u) {
+        if (tiles <= 2) RLE_DEC_ONE(2, 4096);
+        else if (tiles <= 3) RLE_DEC_ONE(3, 4096);
+        else if (tiles <= 5) RLE_DEC_ONE(5, 4096);
+        else RLE_DEC_ONE(8, 4096);
+    } else {
+        if (tiles <= 2) RLE_DEC_ONE(2, 16384);
+        else if (tiles <= 3) RLE_DEC_ONE(3, 16384);
+        else if (tiles <= 5) RLE_DEC_ONE(5, 16384);
+        else if (tiles <= 8) RLE_DEC_ONE(8, 16384);
+        else if (tiles <= 12) RLE_DEC_ONE(12, 16384);
+        else RLE_DEC_ONE(16, 16384);
+    }
+#undef RLE_DEC_ONE
+#undef RLE_DEC_ONE_R
     return hipGetLastError() == hipSuccess ? 1 : RLE_E_HIP;
 }
 

@@ -1275,6 +1275,16 @@ void svc_unregister(Ctx*) {}
 void svc_stop() {}
 #endif  // RLE_VARIANTS (resident service)
 
+}  // namespace
+
+// One buffer with its sizes as kernel arguments (csrc/rle_coop.hip): 1 launched, 0 not qualifying
+// (the batched entry points are used), < 0 a launch error.
+extern "C" int rle_encode_coop_one(const void* src, void* dst, uint64_t U, uint64_t* d_out_len, uint32_t* d_status,
+                                   uint32_t flags, void* stream);
+extern "C" int rle_decode_coop_one(const void* src, void* dst, uint64_t C, uint64_t U, uint64_t cap,
+                                   uint32_t* d_status, uint32_t flags, void* stream);
+
+namespace {
 char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSize) {
     uint8_t* h = zc(c);
     memcpy(h + kZcIn, data, U);
@@ -1306,7 +1316,13 @@ char* compress_small_zc(Ctx* c, const char* data, size_t U, size_t* compressedSi
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = kPending;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-        if (rle_encode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
+        // the sizes by value where the cooperative kernels take the buffer: its first loads do not
+        // wait for the launch words to come over PCIe
+        const int one = rle_encode_coop_one(c->d_zc + kZcIn, c->d_zc + kZcOut, U, dw + 3,
+                                            reinterpret_cast<uint32_t*>(dw + 4), zc_flags(), c->s);
+        if (one < 0) die("encode launch", hipGetLastError());
+        if (one == 0 &&
+            rle_encode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3,
                                                 reinterpret_cast<uint32_t*>(dw + 4), 1, U, zc_flags(), c->s) != RLE_OK)
             die("encode launch", hipGetLastError());
         check_encode_status(zc_wait(c, hw + 4));
@@ -1348,7 +1364,11 @@ void decompress_small_zc(Ctx* c, const char* data, size_t C, size_t U, size_t E,
         uint64_t* hw = reinterpret_cast<uint64_t*>(h + kZcWords);
         hw[0] = kZcIn; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = kPending;
         uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
-        if (rle_decode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
+        const int one = rle_decode_coop_one(c->d_zc + kZcIn, c->d_zc + kZcOut, C, U, total,
+                                            reinterpret_cast<uint32_t*>(dw + 5), zc_flags(), c->s);
+        if (one < 0) die("decode launch", hipGetLastError());
+        if (one == 0 &&
+            rle_decode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc + kZcOut, dw + 2, dw + 3, dw + 4,
                                                 reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, zc_flags(), c->s) != RLE_OK)
             die("decode launch", hipGetLastError());
         st = zc_wait(c, hw + 5);
@@ -1540,11 +1560,18 @@ char* append_small_zc(Ctx* c, const char* content, size_t C, size_t U, const cha
     uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
     hw[0] = kZcIn; hw[1] = C; hw[2] = kZcOut; hw[3] = U; hw[4] = U; hw[5] = kPending;           // decode
     hw[6] = kZcOut; hw[7] = U + A; hw[8] = kZcIn; hw[9] = 0; hw[10] = kPending;                // encode
-    if (rle_decode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc, dw + 2, dw + 3, dw + 4,
-                                            reinterpret_cast<uint32_t*>(dw + 5), 1, C, U, zc_flags(), c->s) != RLE_OK)
+    // (the sizes by value where the cooperative kernels take them, as compress_small_zc)
+    const int d1 = rle_decode_coop_one(c->d_zc + kZcIn, c->d_zc + kZcOut, C, U, U,
+                                       reinterpret_cast<uint32_t*>(dw + 5), zc_flags(), c->s);
+    if (d1 < 0 || (d1 == 0 && rle_decode_batch_device_sized_flags(c->d_zc, dw + 0, dw + 1, c->d_zc, dw + 2, dw + 3,
+                                                                   dw + 4, reinterpret_cast<uint32_t*>(dw + 5), 1, C,
+                                                                   U, zc_flags(), c->s) != RLE_OK))
         die("decode launch", hipGetLastError());
-    if (rle_encode_batch_device_sized_flags(c->d_zc, dw + 6, dw + 7, c->d_zc, dw + 8, dw + 9,
-                                            reinterpret_cast<uint32_t*>(dw + 10), 1, U + A, zc_flags(), c->s) != RLE_OK)
+    const int e1 = rle_encode_coop_one(c->d_zc + kZcOut, c->d_zc + kZcIn, U + A, dw + 9,
+                                       reinterpret_cast<uint32_t*>(dw + 10), zc_flags(), c->s);
+    if (e1 < 0 || (e1 == 0 && rle_encode_batch_device_sized_flags(c->d_zc, dw + 6, dw + 7, c->d_zc, dw + 8, dw + 9,
+                                                                   reinterpret_cast<uint32_t*>(dw + 10), 1, U + A,
+                                                                   zc_flags(), c->s) != RLE_OK))
         die("encode launch", hipGetLastError());
     check_encode_status(zc_wait(c, hw + 10));
     const uint32_t st = __atomic_load_n(reinterpret_cast<const uint32_t*>(hw + 5), __ATOMIC_ACQUIRE);

@@ -372,16 +372,20 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("poll,service,zcseg", [("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("1", "0", "8192")])
-def test_polled_small_calls_bit_exact(poll, service, zcseg):
+@pytest.mark.parametrize("poll,service,zcseg,one", [("1", "0", "0", "1"), ("0", "0", "0", "1"), ("1", "1", "0", "1"),
+                                                    ("1", "0", "8192", "1"), ("1", "0", "0", "0")])
+def test_polled_small_calls_bit_exact(poll, service, zcseg, one):
     """The zero-copy small calls' completion: polling the status word the kernel stores behind a
     system-scope release (RLE_MI355X_POLL=1, the default) or hipStreamSynchronize (=0), or the
     resident service (RLE_MI355X_SERVICE=1: no launch per call, csrc/rle_service.h; built into the
     RLE_VARIANTS test library only since round 5, so that case loads it).  600
     consecutive calls of 0-16 KiB (cooperative and one-wave kernels), decodes with an extra region,
     serial-path streams, then 8 threads x 150 round trips, all against the oracle.  zcseg: calls
-    from that many bytes run the segmented kernels on the mapped buffer (RLE_MI355X_ZC_SEG)."""
-    env = dict(os.environ, RLE_MI355X_POLL=poll, RLE_MI355X_SERVICE=service, RLE_MI355X_ZC_SEG=zcseg)
+    from that many bytes run the segmented kernels on the mapped buffer (RLE_MI355X_ZC_SEG).  one:
+    the cooperative kernels take a single call's sizes as arguments (RLE_MI355X_COOP_ONE=1, the
+    default since round 6) or read them from the mapped launch words (=0, the batched entry points)."""
+    env = dict(os.environ, RLE_MI355X_POLL=poll, RLE_MI355X_SERVICE=service, RLE_MI355X_ZC_SEG=zcseg,
+               RLE_MI355X_COOP_ONE=one)
     if service == "1":
         env["RLE_MI355X_LIB"] = VARIANTS_LIB
     r = subprocess.run([sys.executable, "-c", _POLL_CODE, os.path.join(ROOT, "c-filestorage-server-and-client_amd"),
