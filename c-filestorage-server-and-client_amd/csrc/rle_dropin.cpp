@@ -1484,6 +1484,21 @@ int rle_append_prepare_launch(const void* d_mid, uint64_t U, void* d_head, unsig
                               uint64_t* d_res, hipStream_t s);   // csrc/rle_fileops.hip
 int rle_copy_len_launch(void* dst, const void* src, const uint64_t* d_len, uint64_t max_bytes,
                         hipStream_t s);                          // csrc/rle_kernels.hip
+int rle_copy_in_launch(void* dst, const void* src, uint64_t n, hipStream_t s);   // csrc/rle_kernels.hip
+
+namespace {
+// A registered call's input: read by a copy kernel through its device address when it is 16-byte
+// aligned (the kernels after it start sooner than after a DMA, rle_kernels.hip copy_in_kernel), the
+// DMA otherwise.  (A/B) RLE_MI355X_REG_KREAD=0: always the DMA.
+const bool g_reg_kread = [] {
+    const char* e = getenv("RLE_MI355X_REG_KREAD");
+    return e ? atoi(e) != 0 : true;
+}();
+void reg_input(Ctx* c, const LargeCall& lc, const char* data, size_t n) {
+    if (g_reg_kread && rle_copy_in_launch(c->d_in, lc.d_in, n, c->s) == RLE_OK) return;
+    check(hipMemcpyAsync(c->d_in, data, n, hipMemcpyHostToDevice, c->s), "H2D");
+}
+}  // namespace
 
 namespace {
 // RLEappend of a small file (old stream decoded by one wave, c^r ‖ new encoded by one wave, output
@@ -1635,7 +1650,7 @@ char* compress_registered(Ctx* c, const LargeCall& lc, const char* data, size_t 
     uint64_t* hw = reinterpret_cast<uint64_t*>(c->h_zc + kZcWords);
     uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
     hw[0] = 0; hw[1] = U; hw[2] = 0; hw[3] = 0; hw[4] = 0;
-    check(hipMemcpyAsync(c->d_in, data, U, hipMemcpyHostToDevice, c->s), "H2D");
+    reg_input(c, lc, data, U);
     if (rle_encode_batch_device_seg(c->d_in, dw + 0, dw + 1, c->d_out, dw + 2, dw + 3, reinterpret_cast<uint32_t*>(dw + 4),
                                     1, U, c->d_ws, c->d_ws_cap, c->s) != RLE_OK)
         die("encode launch", hipGetLastError());
@@ -1720,7 +1735,7 @@ void decompress_registered(Ctx* c, const LargeCall& lc, const char* data, size_t
     uint64_t* hw = reinterpret_cast<uint64_t*>(c->h_zc + kZcWords);   // (launch words: compress_registered)
     uint64_t* dw = reinterpret_cast<uint64_t*>(c->d_zc + kZcWords);
     hw[0] = 0; hw[1] = C; hw[2] = 0; hw[3] = U; hw[4] = total; hw[5] = 0;
-    check(hipMemcpyAsync(c->d_in, data, C, hipMemcpyHostToDevice, c->s), "H2D");
+    reg_input(c, lc, data, C);
     uint32_t* d_status = reinterpret_cast<uint32_t*>(dw + 5);
     const int drc = C >= kSegDecodeBytes
                         ? rle_decode_batch_device_seg(c->d_in, dw + 0, dw + 1, c->d_out, dw + 2, dw + 3, dw + 4, d_status,

@@ -938,7 +938,46 @@ __global__ __launch_bounds__(256) void copy_len_kernel(uint8_t* __restrict__ dst
         reinterpret_cast<u32x4*>(dst)[i] = reinterpret_cast<const u32x4*>(src)[i];
     if (blockIdx.x == 0 && threadIdx.x < (uint32_t)(n & 15u)) dst[16u * n16 + threadIdx.x] = src[16u * n16 + threadIdx.x];
 }
+// Host path (registered calls, round 6): the caller's n input bytes, registered for the call, read
+// over PCIe through their device address into device memory.  It replaces the DMA: the kernels after
+// it start about 1 µs after it ends, against about 10 µs after a DMA (tools/probes/
+// hostpath_kread_probe.hip, r6ax: 1 MiB 38.5 against 42.8 µs with a kernel after each).  Four 16-byte
+// loads in flight per lane, the last n % 16 bytes one by one (nothing past src + n is read).
+__global__ __launch_bounds__(256) void copy_in_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
+                                                      uint64_t n) {
+    const uint64_t n16 = n / 16u, stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3u * stride < n16; i += 4u * stride) {
+        const u32x4 a = src[i], b = src[i + stride], c = src[i + 2u * stride], d = src[i + 3u * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2u * stride] = c;
+        dst[i + 3u * stride] = d;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < (uint32_t)(n & 15u))
+        reinterpret_cast<uint8_t*>(dst)[16u * n16 + threadIdx.x] =
+            reinterpret_cast<const uint8_t*>(src)[16u * n16 + threadIdx.x];
+}
 }  // namespace rle
+
+// (csrc/rle_dropin.cpp) dst and src 16-byte aligned (else RLE_E_INVAL: the caller takes the DMA)
+int rle_copy_in_launch(void* dst, const void* src, uint64_t n, hipStream_t s) {
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15u) != 0) return RLE_E_INVAL;
+    if (n == 0) return RLE_OK;
+    // At most 64 workgroups (1 MiB of loads in flight): more outstanding reads over PCIe were slower
+    // (r6az probe: 4 MiB 107.5 µs at 64, 122.7-123.7 at 256-1024; 1 MiB 37.7 against 38.4-39.3).
+    // RLE_MI355X_KREAD_GRID overrides the cap (A/B).
+    static const uint64_t cap = [] {
+        const char* e = getenv("RLE_MI355X_KREAD_GRID");
+        const long v = e ? atol(e) : 64;
+        return (uint64_t)(v >= 1 && v <= 4096 ? v : 64);
+    }();
+    const uint64_t want = (n / 16u + 1023u) / 1024u;   // (four chunks per lane)
+    const uint32_t grid = (uint32_t)(want < 1u ? 1u : (want < cap ? want : cap));
+    hipLaunchKernelGGL(rle::copy_in_kernel, dim3(grid), dim3(256), 0, s, (rle::u32x4*)dst, (const rle::u32x4*)src, n);
+    return hipGetLastError() == hipSuccess ? RLE_OK : RLE_E_HIP;
+}
 
 // (csrc/rle_dropin.cpp) dst and src 16-byte aligned, *d_len <= max_bytes
 int rle_copy_len_launch(void* dst, const void* src, const uint64_t* d_len, uint64_t max_bytes, hipStream_t s) {

@@ -19,6 +19,10 @@ WL = {  # workload: (buffers, tiles per buffer for decode (1008 B over C), for e
     "k64_runs50": (16384, 66, 64),
     "k64_runs90": (16384, 31, 64),
     "cfg1": (4096, 3.5, 4),   # random 5 / zero 2 decode tiles; 4 encode tiles (1024 B)
+    # configs[2]'s 1 MiB end (the segmented kernels; C / 1008 decode tiles per buffer)
+    "m1_zero": (1024, 347, 1024),
+    "m1_random": (1024, 1044, 1024),
+    "m1_runs50": (1024, 1056, 1024),
 }
 SIMDS = 1024
 
