@@ -24,6 +24,17 @@
 
 namespace rle {
 
+// The decode summary's phase-free count of literal tiles (dec_count_phasefree, round 6): off.  r6be /
+// r6bf, rocprof medians of the summary kernel (1024 x 1 MiB random / runs50 / configs[2] mixed):
+// tried on every tile 236.1 / 364.9 / 80.3 µs, with the back-off below 256.7 / 291.1 / 70.7, off
+// 268.2-269.7 / 269.4-276.5 / 63.6-66.0.  The random gain does not pay for the run-heavy loss.
+#ifndef RLE_SEG_PHASEFREE
+#define RLE_SEG_PHASEFREE 0
+#endif
+#ifndef RLE_SEG_PF_WAIT
+#define RLE_SEG_PF_WAIT 8
+#endif
+
 // Segment length: seg_tiles tiles of 1008 input bytes, a kernel argument chosen by the launcher
 // (4..16 tiles: about 16 segments per CU over the batch).
 #ifndef RLE_SEG_TILES_MAX   // 16 since r3s (was 64): more, shorter segments fill the chip better
@@ -760,6 +771,53 @@ __device__ __forceinline__ u32 dec_count_literal(const DecPrep& pr, u32 d, u32 l
     return kLane ? (u32)__builtin_popcount(K) : wave_sum((u32)__builtin_popcount(K));
 }
 
+// Decoded bytes of a non-tail tile of a literal stream, for every entry phase at once (round 6,
+// the summary pass is VALU-bound, 137 VALU per random tile, profiles/
+// r6bd_seg_sq_kinds.md).  Let EQ(j) be y[j] == y[j + 1].  When every EQ position j also has
+// y[j + 1] != y[j + 2] and y[j + 2] == '2', then (whatever the entry phase d):
+//   * no byte '2' is EQ (y[j + 1] would be '2' and differ from y[j + 2] == '2');
+//   * from d on, every EQ position is a token start, i.e. a "v v 2" pair: the pair's second byte
+//     is not EQ (y[j + 1] != y[j + 2]) nor is its '2', so nothing inside a pair is EQ, and a byte is
+//     a one-byte token exactly where it is neither EQ nor inside a pair;
+//   * positions 0 and 1 are required not EQ: below d they hold the end of a pair the previous tile
+//     started, whose digit may be anything;
+// so the tile decodes to (1008 - #EQ) - d + e bytes and leaves exit phase e = 2 / 1 / 0 for a pair
+// at 1007 / 1006 / neither, the same for every d.  No phase table, no phase scan.  Returns the
+// lane's count of non-EQ positions (0 on the lookahead lane) and e, or kNotFast when a position
+// breaks the condition (the caller then takes dec_prepare and the general path).
+constexpr u32 kEqBad = (~0xF0u & (~0xCCu | 0xAAu)) & 0xFFu;   // bitop3: ~a & (~b | c)
+__device__ __forceinline__ u32 dec_count_phasefree(const u32x4 cur, u32 lane, const DecK& kc, u32& e) {
+    constexpr uint64_t kOwned = (1ull << kOwnLanes) - 1ull;
+    const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+    const u32 la = from_next_lane(w[0], 0u);
+    const u32 nb[4] = {alignbyte(w[1], w[0], 1), alignbyte(w[2], w[1], 1), alignbyte(w[3], w[2], 1),
+                       alignbyte(la, w[3], 1)};
+    const u32 dg[4] = {alignbyte(w[1], w[0], 2), alignbyte(w[2], w[1], 2), alignbyte(w[3], w[2], 2),
+                       alignbyte(la, w[3], 2)};
+    const u32 K80 = kc.K80, K7F = kc.K7F;
+    u32 ne[4];   // 0x80 per byte: y[j] != y[j + 1]
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 t = w[k] ^ nb[k];
+        ne[k] = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(t & K7F), t, K80);
+    }
+    const u32 nn = from_next_lane(ne[0], K80);   // the next lane's first positions
+    u32 bad = 0u, cnt = 0u;
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 nen = alignbyte(k < 3u ? ne[k + 1u] : nn, ne[k], 1);   // y[j + 1] != y[j + 2]
+        const u32 b = dg[k] ^ 0x32323232u;
+        const u32 nd = bitop3<kOrAnd>(faddi<0x7F7F7F7Fu>(b & K7F), b, K80);   // y[j + 2] != '2'
+        bad |= bitop3<kEqBad>(ne[k], nen, nd);   // EQ without NE(j + 1), or with a digit other than '2'
+        cnt += (u32)__builtin_popcount(ne[k]);
+    }
+    if (__builtin_amdgcn_ballot_w64((bad & K80) != 0u) & kOwned) return kNotFast;
+    if ((readlane(ne[0], 0) & 0x8080u) != 0x8080u) return kNotFast;   // EQ at position 0 or 1
+    const u32 ne62 = readlane(ne[3], kOwnLanes - 1u);   // positions 1004..1007
+    e = !(ne62 & 0x80000000u) ? 2u : (!(ne62 & 0x00800000u) ? 1u : 0u);
+    return lane < kOwnLanes ? cnt : 0u;
+}
+
 // One segment's decode summary: for each entry phase 0..2, the decoded bytes (.x .y .z) and, in .w,
 // the exit phases (2 bits each) and the phases whose tiled path declines (bits 8..10).  C > 0.
 // Whether every token starting in this tile (entry phase d, starts S80 from dec_lengths) carries
@@ -788,11 +846,34 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
     u32 uni = 7u, v0 = 0u, v1 = 0u, v2 = 0u;   // single-byte phases and their bytes
     u32 accm = 0u;       // the lane's decoded bytes over the tiles after the phases merged (summed once)
     bool badl = false;   // ... and whether the lane declined in one of them
+    u32 a0 = 0u, a1 = 0u, a2 = 0u;   // phase-free tiles: e - d per entry phase (wave-uniform, wrapping)
+    constexpr u32 kPfWait = RLE_SEG_PF_WAIT;
+    u32 pf_wait = 0u;
     const DecK kc = dec_k();
     walk_seg<kRes>(rsi, q0, ntiles_for(q1 - q0), lane, slots, [&](u32 t, const uint8_t* cs, const Refill& nx) {
         const u32x4 cur = *reinterpret_cast<const u32x4*>(cs + 16u * lane);
         nx();
-        const DecPrep pr = dec_prepare(cur, q0 + t * kTileStep, C, q1, lane, tbl, kc);
+        const u32 pos = q0 + t * kTileStep;
+        // (dec_prepare's non-tail tiles; after a tile the check declines, the next kPfWait tiles go
+        // straight to the general path: run-heavy and zero-filled streams decline on every tile,
+        // r6be: runs50 summary 276.5 -> 364.9 µs when every tile tried)
+        if (pf_wait) {
+            --pf_wait;
+        } else if (RLE_SEG_PHASEFREE && pos + kSlot + 2u <= q1) {
+            u32 e = 0u;
+            const u32 tot = dec_count_phasefree(cur, lane, kc, e);
+            if (tot == kNotFast) pf_wait = kPfWait;
+            else {
+                accm += tot;
+                a0 += e - d0;
+                a1 += e - d1;
+                a2 += e - d2;
+                d0 = d1 = d2 = e;
+                uni = 0u;   // (as the literal path below)
+                return 0u;
+            }
+        }
+        const DecPrep pr = dec_prepare(cur, pos, C, q1, lane, tbl, kc);
         const u32 m63 = readlane(pr.incl, kOwnLanes - 1u);   // lane 63: lookahead only
         if (d0 == d1 && d1 == d2) {   // the three entry phases have merged: one evaluation
             u32 tot = !pr.tail ? dec_count_literal<true>(pr, d0, lane, kc) : kNotFast;
@@ -842,7 +923,7 @@ __device__ __forceinline__ uint4 dec_seg_summarize(const uint8_t* src, u32 C, u3
         return 0u;
     });
     const u32 cm = wave_sum(accm);
-    c0 += cm; c1 += cm; c2 += cm;
+    c0 += cm + a0; c1 += cm + a1; c2 += cm + a2;
     badm |= __builtin_amdgcn_ballot_w64(badl) ? 7u : 0u;
     return make_uint4(c0, c1, c2, d0 | (d1 << 2) | (d2 << 4) | (badm << 8) | (uni << 11));
 }

@@ -25,6 +25,7 @@ WL = {  # workload: (buffers, tiles per buffer for decode (1008 B over C), for e
     "m1_runs50": (1024, 1056, 1024),
 }
 SIMDS = 1024
+KERNELS = ("encode_kernel", "decode_kernel", "enc_seg_", "dec_seg_")   # (with --seg: the segmented passes)
 
 
 def kname(k):
@@ -53,7 +54,7 @@ def main():
         g, dur = collections.defaultdict(float), {}
         for r in csv.DictReader(open(pmc)):
             k = kname(r["Kernel_Name"])
-            if not (k.startswith("encode_kernel") or k.startswith("decode_kernel")):
+            if not k.startswith(KERNELS):
                 continue
             if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
                 g[r["Dispatch_Id"]] += float(r["Counter_Value"])
@@ -72,7 +73,7 @@ def main():
         pdur = collections.defaultdict(dict)
         for r in csv.DictReader(open(pmc)):
             k = kname(r["Kernel_Name"])
-            if not (k.startswith("encode_kernel") or k.startswith("decode_kernel")):
+            if not k.startswith(KERNELS):
                 continue
             key = (r["Dispatch_Id"])
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
